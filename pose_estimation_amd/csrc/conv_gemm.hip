@@ -1,0 +1,291 @@
+// Implicit-GEMM convolution / GEMM on the gfx950 f32 matrix cores.
+//
+// One kernel serves every dense contraction on the KRRN path (SURVEY §8a rows H1-H8,
+// D1-D2, the GCN `feature_map @ weights` of G6/G7 and the TBase Conv1d chain P1):
+//
+//   out[m, n] = act( scale[n] * sum_k A[m, k] * W[n, k] + bias[n] + bias2[m / b2_div, n]
+//                    + res[m, n] )
+//
+// with A the im2col view of an NHWC activation that is never materialised:
+//   m = (b, gy, gx) over a B x Hg x Wg grid, k = (tap, c) over ntaps x cin,
+//   A[m, (tap, c)] = in[b, gy*in_s + dy[tap], gx*in_s + dx[tap], c]   (0 outside)
+// and the output pixel of grid point (gy, gx) is (gy*osy + ooy, gx*osx + oox).
+// A stride-s conv is in_s = s with taps (ky-p, kx-p); a stride-2 transposed conv is
+// four launches (one per output parity class) with in_s = 1, osy = osx = 2 and the
+// class's 1..4 taps (sub-pixel decomposition), so no zero-inserted input exists.
+//
+// Numerics: operands stay f32 and are multiplied on v_mfma_f32_32x32x2_f32, which is
+// bit-for-bit a k-ordered fmaf chain (cdna_hip_programming.md §3 "FP32-input MFMA").
+// The reference path evaluates in f32 (tools/trainer.py:466-475 has no autocast at
+// eval), so this is the reference precision, not a reduced one.
+//
+// Tiling (MI355X-first):
+//   * block = 256 threads = 4 waves as 2(M) x 2(N); block tile BM x BN, BK = 16;
+//   * both LDS tiles are k-contiguous ([row][k], row pitch 20 floats): lane half h of
+//     MFMA step j reads k = 8*(j/4) + 4h + (j%4), so one ds_read_b128 feeds 4 MFMAs
+//     and the pitch 20 (5 x 16 B) makes every 16-lane ds_read_b128 group hit 16
+//     distinct 16-B bank slots (5 is odd => r*5 mod 16 is a bijection): conflict-free;
+//   * global->register staging of tile k+1 overlaps the MFMAs of tile k (double
+//     buffered LDS, one barrier per k-tile);
+//   * blockIdx is remapped XCD-aware so tiles that share an A panel share an L2.
+// NCHW=true swaps the MFMA operands (C^T) so the lane index runs over pixels and the
+// store into an NCHW tensor is coalesced (used for the heads' final 1x1 convs, whose
+// outputs are the NCHW `xyz/mask/region/normal` maps of KRRN.forward, krrn.py:100-108).
+#include "krrn_common.h"
+
+namespace {
+
+constexpr int kBK = 16;
+constexpr int kPitch = 20;  // floats per LDS row (16 + 4 pad)
+
+struct ConvArgs {
+  const float* in;
+  int in_cs, in_co;
+  int B, Hi, Wi;
+  int cin;  // physical channels per tap (multiple of 4)
+  int Hg, Wg, in_s;
+  int ntaps;
+  int dy[9];
+  int dx[9];
+  const float* wt;  // [N][K] row-major, K = ntaps * cin
+  int K, N, n_store;
+  const float* scale;
+  const float* bias;
+  const float* bias2;
+  int b2_div;
+  const float* res;
+  int res_cs, res_co;
+  float* out;
+  int out_cs, out_co;
+  int Ho, Wo, osy, osx, ooy, oox;
+  int relu;
+  int M;
+};
+
+template <int BM, int BN, bool NCHW>
+__global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int MI = WM / 32, NI = WN / 32;
+  constexpr int AL = BM / 64, BL = BN / 64;  // float4 staged per thread
+  constexpr int A_FLOATS = BM * kPitch, B_FLOATS = BN * kPitch;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (A_FLOATS + B_FLOATS)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int n_tiles = (a.N + BN - 1) / BN;
+  const int m_tiles = (a.M + BM - 1) / BM;
+  const int bid = krrn_xcd_remap(blockIdx.x, m_tiles * n_tiles);
+  const int tm = bid / n_tiles, tn = bid % n_tiles;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread staging geometry -------------------------------------------------
+  const int srow = tid >> 2;       // 0..63
+  const int kq = (tid & 3) * 4;    // k offset inside the tile
+  const int HWg = a.Hg * a.Wg;
+  const float* a_base[AL];
+  int a_iy[AL], a_ix[AL];
+  bool a_ok[AL];
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int m = m0 + srow + 64 * i;
+    a_ok[i] = m < a.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int b = mm / HWg;
+    const int r = mm - b * HWg;
+    const int gy = r / a.Wg, gx = r - (r / a.Wg) * a.Wg;
+    a_iy[i] = gy * a.in_s;
+    a_ix[i] = gx * a.in_s;
+    a_base[i] = a.in + (size_t)b * a.Hi * a.Wi * a.in_cs + a.in_co;
+  }
+  // (tap, c) of this thread's first k; advanced by kBK per tile
+  int tap = kq / a.cin;
+  int cc = kq - tap * a.cin;
+  int kk = kq;  // absolute k of this thread's staged float4
+
+  f32x4 ra[AL], rb[BL];
+
+  auto load_tile = [&]() {
+    int ddy = 0, ddx = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t == tap) { ddy = a.dy[t]; ddx = a.dx[t]; }
+    }
+    const bool tap_ok = tap < a.ntaps;
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+      const int iy = a_iy[i] + ddy, ix = a_ix[i] + ddx;
+      const bool ok = a_ok[i] && tap_ok && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+      if (ok) {
+        ra[i] = *reinterpret_cast<const f32x4*>(a_base[i] + ((size_t)iy * a.Wi + ix) * a.in_cs + cc);
+      } else {
+        ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int n = n0 + srow + 64 * i;
+      if (n < a.N && kk < a.K) {
+        rb[i] = *reinterpret_cast<const f32x4*>(a.wt + (size_t)n * a.K + kk);
+      } else {
+        rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    // advance to the next k-tile
+    kk += kBK;
+    cc += kBK;
+    while (cc >= a.cin) { cc -= a.cin; ++tap; }
+  };
+  auto store_tile = [&](int buf) {
+    float* As = smem + buf * (A_FLOATS + B_FLOATS);
+    float* Bs = As + A_FLOATS;
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+      *reinterpret_cast<f32x4*>(As + (srow + 64 * i) * kPitch + kq) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BL; ++i)
+      *reinterpret_cast<f32x4*>(Bs + (srow + 64 * i) * kPitch + kq) = rb[i];
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nkt = (a.K + kBK - 1) / kBK;
+  load_tile();
+  store_tile(0);
+  __syncthreads();
+
+  const int frow = lane & 31, fh = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) load_tile();
+    const float* As = smem + cur * (A_FLOATS + B_FLOATS);
+    const float* Bs = As + A_FLOATS;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      f32x4 af[MI], bf[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        af[i] = *reinterpret_cast<const f32x4*>(As + (wm * WM + i * 32 + frow) * kPitch + g * 8 + 4 * fh);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        bf[j] = *reinterpret_cast<const f32x4*>(Bs + (wn * WN + j * 32 + frow) * kPitch + g * 8 + 4 * fh);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            if constexpr (NCHW)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(bf[j][s], af[i][s], acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+          }
+    }
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue -----------------------------------------------------------------------
+  const int HWo = a.Ho * a.Wo;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      if constexpr (!NCHW) {
+        const int n = n0 + wn * WN + j * 32 + frow;
+        if (n >= a.n_store) continue;
+        const float sc = a.scale ? a.scale[n] : 1.f;
+        const float bi = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          if (m >= a.M) continue;
+          const int b = m / HWg;
+          const int rr = m - b * HWg;
+          const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
+          const int oy = gy * a.osy + a.ooy, ox = gx * a.osx + a.oox;
+          const size_t pix = ((size_t)b * a.Ho + oy) * a.Wo + ox;
+          float v = acc[i][j][r] * sc + bi;
+          if (a.bias2) v += a.bias2[(size_t)(m / a.b2_div) * a.N + n];
+          if (a.res) v += a.res[pix * a.res_cs + a.res_co + n];
+          if (a.relu) v = fmaxf(v, 0.f);
+          a.out[pix * a.out_cs + a.out_co + n] = v;
+        }
+      } else {
+        const int m = m0 + wm * WM + i * 32 + frow;
+        if (m >= a.M) continue;
+        const int b = m / HWg;
+        const int rr = m - b * HWg;
+        const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
+        const int oy = gy * a.osy + a.ooy, ox = gx * a.osx + a.oox;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int n = n0 + wn * WN + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          if (n >= a.n_store) continue;
+          float v = acc[i][j][r] * (a.scale ? a.scale[n] : 1.f) + (a.bias ? a.bias[n] : 0.f);
+          if (a.bias2) v += a.bias2[(size_t)(m / a.b2_div) * a.N + n];
+          if (a.relu) v = fmaxf(v, 0.f);
+          a.out[((size_t)b * a.out_cs + a.out_co + n) * HWo + (size_t)oy * a.Wo + ox] = v;
+        }
+      }
+    }
+}
+
+template <int BM, int BN, bool NCHW>
+int launch(const ConvArgs& a, hipStream_t s) {
+  const int nwg = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
+  hipLaunchKernelGGL((conv_gemm_f32_kernel<BM, BN, NCHW>), dim3(nwg), dim3(256), 0, s, a);
+  return krrn_launch_status();
+}
+
+}  // namespace
+
+// C-ABI: see include/krrn_hip.h for the argument contract.
+KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin,
+                             int Hg, int Wg, int in_s, int ntaps, const int* tap_dy, const int* tap_dx,
+                             const float* wt, int N, int n_store, const float* scale, const float* bias,
+                             const float* bias2, int b2_div, const float* res, int res_cs, int res_co,
+                             float* out, int out_cs, int out_co, int Ho, int Wo, int osy, int osx, int ooy,
+                             int oox, int relu, int out_nchw, int tile, void* stream) {
+  if (!in || !wt || !out || !tap_dy || !tap_dx) return KRRN_EARG;
+  if (ntaps < 1 || ntaps > 9 || B < 1 || Hi < 1 || Wi < 1 || Hg < 1 || Wg < 1 || N < 1) return KRRN_ESHAPE;
+  if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(in) || !krrn_aligned16(wt)) return KRRN_EALIGN;
+  if (n_store < 1 || n_store > N) return KRRN_ESHAPE;
+  if (bias2 && b2_div < 1) return KRRN_EARG;
+  if (!out_nchw && out_co + n_store > out_cs) return KRRN_ESHAPE;
+  const long long M = (long long)B * Hg * Wg;
+  if (M > 0x7fffffffLL) return KRRN_ESHAPE;
+  ConvArgs a;
+  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.Hi = Hi; a.Wi = Wi; a.cin = cin;
+  a.Hg = Hg; a.Wg = Wg; a.in_s = in_s; a.ntaps = ntaps;
+  for (int t = 0; t < 9; ++t) { a.dy[t] = t < ntaps ? tap_dy[t] : 0; a.dx[t] = t < ntaps ? tap_dx[t] : 0; }
+  a.wt = wt; a.K = ntaps * cin; a.N = N; a.n_store = n_store;
+  a.scale = scale; a.bias = bias; a.bias2 = bias2; a.b2_div = b2_div > 0 ? b2_div : 1;
+  a.res = res; a.res_cs = res_cs; a.res_co = res_co;
+  a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.Ho = Ho; a.Wo = Wo;
+  a.osy = osy; a.osx = osx; a.ooy = ooy; a.oox = oox; a.relu = relu; a.M = (int)M;
+  hipStream_t s = (hipStream_t)stream;
+  // tile: 0 = auto, 1 = 128x128, 2 = 128x64, 3 = 64x64
+  if (tile == 0) {
+    const long long wg128 = (long long)krrn_cdiv(a.M, 128) * krrn_cdiv(N, 128);
+    if (N <= 64) tile = (krrn_cdiv(a.M, 128) >= 512) ? 2 : 3;
+    else tile = (wg128 >= 512) ? 1 : 3;
+  }
+  if (out_nchw) {
+    if (tile == 1) return launch<128, 128, true>(a, s);
+    if (tile == 2) return launch<128, 64, true>(a, s);
+    return launch<64, 64, true>(a, s);
+  }
+  if (tile == 1) return launch<128, 128, false>(a, s);
+  if (tile == 2) return launch<128, 64, false>(a, s);
+  return launch<64, 64, false>(a, s);
+}

@@ -1,0 +1,247 @@
+"""Thin Python wrappers over the C-ABI entry points of libkrrn_hip.so.
+
+Tensors are used only as device-memory handles: every wrapper passes raw
+``data_ptr()`` values, sizes and the current HIP stream to the library. No
+arithmetic happens here.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _int_array(vals: Sequence[int], n: int = 9):
+    arr = (ctypes.c_int * n)()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
+    return arr
+
+
+def pad4(c: int) -> int:
+    return (c + 3) // 4 * 4
+
+
+@dataclass
+class Act:
+    """An NHWC activation: channels [co, co + cp) of a [B, H, W, cs] f32 buffer.
+
+    ``c`` is the logical channel count (reference layout); ``cp = pad4(c)`` is the
+    physical width the kernels read/write (pad channels are kept at exactly 0).
+    """
+    t: torch.Tensor
+    B: int
+    H: int
+    W: int
+    cs: int
+    co: int
+    c: int
+
+    @property
+    def cp(self) -> int:
+        return pad4(self.c)
+
+    def slice(self, co: int, c: int) -> "Act":
+        return Act(self.t, self.B, self.H, self.W, self.cs, self.co + co, c)
+
+
+def new_act(B: int, H: int, W: int, c: int, device, cs: Optional[int] = None) -> Act:
+    cs = pad4(c) if cs is None else cs
+    t = torch.zeros((B, H, W, cs), dtype=torch.float32, device=device)
+    return Act(t, B, H, W, cs, 0, c)
+
+
+@dataclass
+class ConvSpec:
+    """A folded convolution ready for krrn_conv2d_f32.
+
+    ``wt``: [classes][Np, ntaps*cin_p]; ``taps``/``grid`` describe each launch class.
+    For a plain conv there is one class; a stride-2 transposed conv has four
+    (output parity classes, sub-pixel decomposition).
+    """
+    wt: List[torch.Tensor]
+    taps: List[List[Tuple[int, int]]]
+    cls_off: List[Tuple[int, int]]  # output offset (ooy, oox) per class
+    scale: torch.Tensor
+    bias: torch.Tensor
+    cin_p: int
+    cout: int
+    stride: int      # input stride for normal convs
+    kind: str        # "conv" | "convT"
+    ksize: int
+    pad: int
+
+
+def conv_out_hw(spec: ConvSpec, H: int, W: int) -> Tuple[int, int]:
+    if spec.kind == "conv":
+        Ho = (H + 2 * spec.pad - spec.ksize) // spec.stride + 1
+        Wo = (W + 2 * spec.pad - spec.ksize) // spec.stride + 1
+        return Ho, Wo
+    return 2 * H, 2 * W
+
+
+def conv2d(x: Act, spec: ConvSpec, out: Act, res: Optional[Act] = None, relu: bool = False,
+           bias2: Optional[torch.Tensor] = None, b2_div: int = 1, tile: int = 0):
+    """out = act(BN(conv(x)) [+ bias2] [+ res]) written into ``out``'s channel slice."""
+    assert x.cp == spec.cin_p, (x.c, x.cp, spec.cin_p)
+    Ho, Wo = out.H, out.W
+    np_ = pad4(spec.cout)
+    for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off)):
+        if spec.kind == "conv":
+            Hg, Wg, in_s, osy, osx = Ho, Wo, spec.stride, 1, 1
+        else:
+            Hg, Wg, in_s, osy, osx = x.H, x.W, 1, 2, 2
+        dy = _int_array([t[0] for t in taps])
+        dx = _int_array([t[1] for t in taps])
+        _lib.call("krrn_conv2d_f32",
+                  _ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p,
+                  Hg, Wg, in_s, len(taps), dy, dx,
+                  _ptr(spec.wt[cls]), np_, np_, _ptr(spec.scale), _ptr(spec.bias),
+                  _ptr(bias2), b2_div,
+                  _ptr(res.t if res is not None else None), res.cs if res is not None else 0,
+                  res.co if res is not None else 0,
+                  _ptr(out.t), out.cs, out.co, Ho, Wo, osy, osx, ooy, oox, int(relu), 0, tile, _stream())
+
+
+def conv2d_nchw(x: Act, spec: ConvSpec, out: torch.Tensor, n_store: int, relu: bool = False, tile: int = 0):
+    """Final 1x1 conv writing an NCHW [B, n_store, H, W] tensor (heads, krrn.py:97-98)."""
+    assert spec.kind == "conv" and len(spec.taps) == 1
+    B, C, Ho, Wo = out.shape
+    np_ = pad4(spec.cout)
+    taps = spec.taps[0]
+    _lib.call("krrn_conv2d_f32",
+              _ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p,
+              Ho, Wo, spec.stride, len(taps), _int_array([t[0] for t in taps]), _int_array([t[1] for t in taps]),
+              _ptr(spec.wt[0]), np_, n_store, _ptr(spec.scale), _ptr(spec.bias), _ptr(None), 1,
+              _ptr(None), 0, 0, _ptr(out), C, 0, Ho, Wo, 1, 1, 0, 0, int(relu), 1, tile, _stream())
+
+
+def gemm(a: torch.Tensor, a_cs: int, a_co: int, M: int, spec: ConvSpec, out: torch.Tensor, out_cs: int,
+         out_co: int, relu: bool = False, bias2: Optional[torch.Tensor] = None, b2_div: int = 1, tile: int = 0):
+    """Row-major GEMM out[M, :N] = act(scale * (A[M, K] @ W^T) + bias [+ bias2]) via the conv kernel."""
+    np_ = pad4(spec.cout)
+    _lib.call("krrn_conv2d_f32",
+              _ptr(a), a_cs, a_co, 1, 1, M, spec.cin_p, 1, M, 1, 1, _int_array([0]), _int_array([0]),
+              _ptr(spec.wt[0]), np_, np_, _ptr(spec.scale), _ptr(spec.bias), _ptr(bias2), b2_div,
+              _ptr(None), 0, 0, _ptr(out), out_cs, out_co, 1, M, 1, 1, 0, 0, int(relu), 0, tile, _stream())
+
+
+# ----------------------------------------------------------------------------------------
+# Weight folding / packing (run once at plan build time; not on the per-step path)
+# ----------------------------------------------------------------------------------------
+
+def fold_bn(cout: int, conv_bias: Optional[torch.Tensor], bn: Optional[torch.nn.Module], device):
+    """Eval-mode BN folded to (scale, bias): y = scale * conv + bias (BN eps from the module)."""
+    np_ = pad4(cout)
+    scale = torch.zeros(np_, dtype=torch.float64)
+    bias = torch.zeros(np_, dtype=torch.float64)
+    cb = conv_bias.detach().double().cpu() if conv_bias is not None else torch.zeros(cout, dtype=torch.float64)
+    if bn is None:
+        scale[:cout] = 1.0
+        bias[:cout] = cb
+    else:
+        g = bn.weight.detach().double().cpu()
+        b = bn.bias.detach().double().cpu()
+        mu = bn.running_mean.detach().double().cpu()
+        var = bn.running_var.detach().double().cpu()
+        s = g / torch.sqrt(var + bn.eps)
+        scale[:cout] = s
+        bias[:cout] = (cb - mu) * s + b
+    return scale.float().to(device), bias.float().to(device)
+
+
+def _pack_taps(w: torch.Tensor, taps_k: List[Tuple[int, int]], cin_map: List[int], cin_p: int, cout: int):
+    """w: [cout, cin, kh, kw] (conv layout) -> [pad4(cout), ntaps * cin_p], channel-mapped.
+
+    cin_map[c] = physical channel of logical input channel c.
+    """
+    np_ = pad4(cout)
+    nt = len(taps_k)
+    out = torch.zeros(np_, nt, cin_p, dtype=torch.float32)
+    idx = torch.tensor(cin_map, dtype=torch.long)
+    for t, (ky, kx) in enumerate(taps_k):
+        out[:cout, t, idx] = w[:, :, ky, kx].float()
+    return out.reshape(np_, nt * cin_p).contiguous()
+
+
+def make_conv(conv: torch.nn.Conv2d, bn: Optional[torch.nn.Module], device, cin_map: Optional[List[int]] = None,
+              cin_p: Optional[int] = None) -> ConvSpec:
+    w = conv.weight.detach().cpu()
+    cout, cin, kh, kw = w.shape
+    assert kh == kw
+    k, s = kh, conv.stride[0]
+    p = conv.padding
+    if isinstance(p, str):  # 'same' (stride 1, odd kernel)
+        pad = (k - 1) // 2
+    else:
+        pad = p[0]
+    if cin_map is None:
+        cin_map = list(range(cin))
+    cin_p = pad4(max(cin_map) + 1) if cin_p is None else cin_p
+    taps_k = [(ky, kx) for ky in range(k) for kx in range(k)]
+    wt = _pack_taps(w, taps_k, cin_map, cin_p, cout).to(device)
+    scale, bias = fold_bn(cout, conv.bias, bn, device)
+    taps = [(ky - pad, kx - pad) for (ky, kx) in taps_k]
+    return ConvSpec([wt], [taps], [(0, 0)], scale, bias, cin_p, cout, s, "conv", k, pad)
+
+
+def make_convT(convT: torch.nn.ConvTranspose2d, bn: Optional[torch.nn.Module], device,
+               cin_map: Optional[List[int]] = None, cin_p: Optional[int] = None) -> ConvSpec:
+    """Stride-2 ConvTranspose2d as four parity-class convolutions.
+
+    Output row oy = 2*iy - pad + ky (+ output_padding rows at the end). For parity
+    py = oy % 2, oy = 2a + py, the contributing taps satisfy ky = 2(a - iy) + py + pad,
+    i.e. iy = a + (py + pad - ky) / 2 for every ky with (py + pad - ky) even.
+    """
+    w = convT.weight.detach().cpu()  # [cin, cout, kh, kw]
+    cin, cout, kh, kw = w.shape
+    assert convT.stride[0] == 2 and convT.stride[1] == 2 and kh == kw
+    pad = convT.padding[0]
+    if cin_map is None:
+        cin_map = list(range(cin))
+    cin_p = pad4(max(cin_map) + 1) if cin_p is None else cin_p
+    wc = w.permute(1, 0, 2, 3)  # [cout, cin, kh, kw]
+    wts, taps_all, offs = [], [], []
+    for py in range(2):
+        for px in range(2):
+            taps_k, taps = [], []
+            for ky in range(kh):
+                if (py + pad - ky) % 2:
+                    continue
+                for kx in range(kw):
+                    if (px + pad - kx) % 2:
+                        continue
+                    taps_k.append((ky, kx))
+                    taps.append(((py + pad - ky) // 2, (px + pad - kx) // 2))
+            wts.append(_pack_taps(wc, taps_k, cin_map, cin_p, cout).to(device))
+            taps_all.append(taps)
+            offs.append((py, px))
+    scale, bias = fold_bn(cout, convT.bias, bn, device)
+    return ConvSpec(wts, taps_all, offs, scale, bias, cin_p, cout, 1, "convT", kh, pad)
+
+
+def make_linear(weight: torch.Tensor, bias: Optional[torch.Tensor], bn: Optional[torch.nn.Module], device,
+                cin_map: Optional[List[int]] = None, cin_p: Optional[int] = None) -> ConvSpec:
+    """A [cout, cin] matrix (Conv1d k=1 or GCN weights^T) as a 1-tap conv spec."""
+    w = weight.detach().cpu().float()
+    if w.dim() == 3:
+        w = w[:, :, 0]
+    cout, cin = w.shape
+    if cin_map is None:
+        cin_map = list(range(cin))
+    cin_p = pad4(max(cin_map) + 1) if cin_p is None else cin_p
+    wt = _pack_taps(w[:, :, None, None], [(0, 0)], cin_map, cin_p, cout).to(device)
+    scale, bias_f = fold_bn(cout, bias, bn, device)
+    return ConvSpec([wt], [[(0, 0)]], [(0, 0)], scale, bias_f, cin_p, cout, 1, "conv", 1, 0)

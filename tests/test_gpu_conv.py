@@ -1,0 +1,108 @@
+"""Implicit-GEMM conv kernel vs a plain PyTorch fp32 reference of the same op."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from pose_estimation_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+TOL = dict(rtol=2e-4, atol=2e-4)
+
+
+def _nhwc(x, dev, cs=None, co=0):
+    B, C, H, W = x.shape
+    a = ops.new_act(B, H, W, C, dev, cs=cs)
+    a = a.slice(co, C) if co else a
+    a.t[..., co:co + C] = x.permute(0, 2, 3, 1).to(dev)
+    return a
+
+
+def _bn(c, g):
+    bn = nn.BatchNorm2d(c).eval()
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(c, generator=g))
+        bn.bias.copy_(0.1 * torch.randn(c, generator=g))
+        bn.running_mean.copy_(0.1 * torch.randn(c, generator=g))
+        bn.running_var.copy_(0.5 + torch.rand(c, generator=g))
+    return bn
+
+
+@pytest.mark.parametrize("cin,cout,k,s,H,bias,tile", [
+    (3, 64, 3, 2, 33, False, 0), (64, 64, 3, 2, 60, False, 0), (18, 36, 3, 1, 15, False, 0),
+    (270, 270, 3, 1, 30, True, 1), (256, 18, 3, 1, 30, False, 3), (144, 18, 1, 1, 4, False, 2),
+    (72, 144, 3, 2, 8, False, 3), (128, 128, 3, 1, 61, False, 1)])
+def test_conv_bn_relu_res(dev, cin, cout, k, s, H, bias, tile):
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    B = 3
+    conv = nn.Conv2d(cin, cout, k, s, (k - 1) // 2, bias=bias)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+        if bias:
+            conv.bias.copy_(0.1 * torch.randn(cout, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, H, generator=g)
+    ref = bn(conv(x))
+    res = torch.randn(ref.shape, generator=g)
+    ref = torch.relu(ref + res).detach()
+    spec = ops.make_conv(conv, bn, dev)
+    xa = _nhwc(x, dev)
+    Ho, Wo = ops.conv_out_hw(spec, H, H)
+    out = ops.new_act(B, Ho, Wo, cout, dev, cs=ops.pad4(cout) + 8)
+    ra = _nhwc(res, dev)
+    ops.conv2d(xa, spec, out, res=ra, relu=True, tile=tile)
+    torch.cuda.synchronize()
+    got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, **TOL)
+    # pad channels stay exactly zero
+    assert torch.count_nonzero(out.t[..., cout:]).item() == 0
+
+
+@pytest.mark.parametrize("cin,cout,k,p,op,H", [(398, 128, 4, 1, 0, 30), (128, 128, 3, 1, 1, 30), (20, 12, 4, 1, 0, 7)])
+def test_convT(dev, cin, cout, k, p, op, H):
+    g = torch.Generator().manual_seed(11 + k)
+    convT = nn.ConvTranspose2d(cin, cout, k, 2, p, output_padding=op, bias=False)
+    with torch.no_grad():
+        convT.weight.copy_(0.05 * torch.randn(convT.weight.shape, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(2, cin, H, H, generator=g)
+    ref = torch.relu(bn(convT(x))).detach()
+    spec = ops.make_convT(convT, bn, dev)
+    xa = _nhwc(x, dev)
+    out = ops.new_act(2, 2 * H, 2 * H, cout, dev)
+    ops.conv2d(xa, spec, out, relu=True)
+    torch.cuda.synchronize()
+    got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, **TOL)
+
+
+def test_conv_nchw_out(dev):
+    g = torch.Generator().manual_seed(5)
+    conv = nn.Conv2d(128, 70, 1, 1, 0, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+        conv.bias.copy_(0.1 * torch.randn(70, generator=g))
+    x = torch.randn(2, 128, 37, 37, generator=g)
+    ref = conv(x).detach()
+    spec = ops.make_conv(conv, None, dev)
+    xa = _nhwc(x, dev)
+    out = torch.empty(2, 70, 37, 37, device=dev)
+    ops.conv2d_nchw(xa, spec, out, n_store=70)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, **TOL)
+
+
+def test_gemm_bias2(dev):
+    g = torch.Generator().manual_seed(9)
+    M, K, N, per = 3000, 1280, 1024, 1000
+    a = torch.randn(M, K, generator=g)
+    w = 0.03 * torch.randn(N, K, generator=g)
+    b = 0.1 * torch.randn(N, generator=g)
+    b2 = torch.randn(3, N, generator=g)
+    ref = torch.relu(a @ w.t() + b + b2.repeat_interleave(per, 0))
+    spec = ops.make_linear(w, b, None, dev)
+    out = torch.zeros(M, N, device=dev)
+    ops.gemm(a.to(dev), K, 0, M, spec, out, N, 0, relu=True, bias2=b2.to(dev), b2_div=per)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-4)
