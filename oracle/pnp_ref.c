@@ -1,0 +1,468 @@
+/*
+ * ORACLE — test infrastructure only (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
+ * Never linked into or called by the product path.
+ *
+ * CPU restatement of the pose step of Trainer.get_pose (tools/trainer.py:383-438):
+ *   cv2.solvePnPRansac(obj, img, K, None, flags=SOLVEPNP_EPNP, confidence=0.9999,
+ *                      reprojectionError=1)
+ * OpenCV is a third-party dependency absent from /root/reference (opencv-python,
+ * version unpinned: the reference ships no requirements file). Its published algorithm is
+ * restated here:
+ *   - EPnP (Lepetit, Moreno-Noguer, Fua, IJCV 2009) as structured in OpenCV's epnp.cpp:
+ *     PCA control points, barycentric alphas, M (2n x 12), null space of M^T M (4 smallest
+ *     eigenvectors), L_6x10 / rho, beta approximations 1/2/3 each refined by 5 Gauss-Newton
+ *     steps, R,t by Procrustes, the solution with the smallest mean reprojection error wins;
+ *   - RANSAC with 5-point EPnP hypotheses, inlier test ||proj - img||^2 <= thr^2, best =
+ *     most inliers (first hypothesis wins ties, accepted only with >= 5 inliers, as
+ *     ptsetreg.cpp's `goodCount > max(maxGoodCount, modelPoints - 1)`), then EPnP on all
+ *     inliers of the best hypothesis.
+ * Deliberate, documented differences (DESIGN.md "PnP"): the H hypothesis subsets are given
+ * by the caller (so GPU and oracle score identical subsets) instead of cv::RNG with
+ * adaptive early exit; Procrustes uses the Kabsch det-correction R = U diag(1,1,d) V^T.
+ * PARITY UNPINNED against cv2 itself (not installable here); pinned by known-answer tests
+ * (exact recovery of a known (R, t) on noiseless correspondences, tests/test_oracle_pnp.py).
+ */
+#include <math.h>
+#include <string.h>
+
+#define MAXP 4096
+
+/* ---------------- small dense linear algebra (double) ---------------- */
+
+/* cyclic Jacobi eigen-decomposition of symmetric n x n A (row-major, destroyed);
+ * eigenvalues -> w, eigenvectors -> rows of V (V[i*n + :] is the i-th eigenvector),
+ * sorted by descending eigenvalue. */
+static void jacobi_eig(double* A, int n, double* w, double* V) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0; /* columns = eigvecs during sweep */
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0, tot = 0.0;
+    for (int p = 0; p < n; ++p)
+      for (int q = 0; q < n; ++q) {
+        const double a2 = A[p * n + q] * A[p * n + q];
+        tot += a2;
+        if (p != q) off += a2;
+      }
+    if (off <= 1e-30 * tot || off < 1e-300) break;
+    for (int p = 0; p < n; ++p) {
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = A[p * n + q];
+        if (fabs(apq) < 1e-300) continue;
+        const double app = A[p * n + p], aqq = A[q * n + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < n; ++k) {
+          const double akp = A[k * n + p], akq = A[k * n + q];
+          A[k * n + p] = c * akp - s * akq;
+          A[k * n + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double apk = A[p * n + k], aqk = A[q * n + k];
+          A[p * n + k] = c * apk - s * aqk;
+          A[q * n + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = c * vkp - s * vkq;
+          V[k * n + q] = s * vkp + c * vkq;
+        }
+      }
+    }
+  }
+  /* sort descending, transpose to row eigenvectors */
+  int order[16];
+  for (int i = 0; i < n; ++i) { order[i] = i; w[i] = A[i * n + i]; }
+  for (int i = 0; i < n; ++i)
+    for (int j = i + 1; j < n; ++j)
+      if (w[order[j]] > w[order[i]]) { int tmp = order[i]; order[i] = order[j]; order[j] = tmp; }
+  double Vt[144], ws[16];
+  for (int i = 0; i < n; ++i) {
+    ws[i] = w[order[i]];
+    for (int k = 0; k < n; ++k) Vt[i * n + k] = V[k * n + order[i]];
+  }
+  memcpy(w, ws, sizeof(double) * n);
+  memcpy(V, Vt, sizeof(double) * n * n);
+}
+
+/* least squares min ||A x - b|| for A m x n (m <= 6, n <= 5) via the pseudo-inverse built
+ * from the eigen-decomposition of A^T A (SVD: A^T A = V S^2 V^T). */
+static void lsq_solve(const double* A, int m, int n, const double* b, double* x) {
+  double AtA[25], w[5], V[25], Atb[5];
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < n; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < m; ++k) s += A[k * n + i] * A[k * n + j];
+      AtA[i * n + j] = s;
+    }
+    double s = 0.0;
+    for (int k = 0; k < m; ++k) s += A[k * n + i] * b[k];
+    Atb[i] = s;
+  }
+  jacobi_eig(AtA, n, w, V);
+  const double tol = (w[0] > 0 ? w[0] : 0.0) * 1e-24;
+  for (int j = 0; j < n; ++j) x[j] = 0.0;
+  for (int i = 0; i < n; ++i) {
+    if (w[i] <= tol) continue;
+    double proj = 0.0;
+    for (int k = 0; k < n; ++k) proj += V[i * n + k] * Atb[k];
+    proj /= w[i];
+    for (int k = 0; k < n; ++k) x[k] += proj * V[i * n + k];
+  }
+}
+
+/* 3x3 inverse via the adjugate (CC is well conditioned by construction: PCA axes) */
+static int inv3(const double* a, double* r) {
+  const double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) +
+                     a[2] * (a[3] * a[7] - a[4] * a[6]);
+  if (fabs(det) < 1e-300) return 0;
+  const double id = 1.0 / det;
+  r[0] = (a[4] * a[8] - a[5] * a[7]) * id;
+  r[1] = (a[2] * a[7] - a[1] * a[8]) * id;
+  r[2] = (a[1] * a[5] - a[2] * a[4]) * id;
+  r[3] = (a[5] * a[6] - a[3] * a[8]) * id;
+  r[4] = (a[0] * a[8] - a[2] * a[6]) * id;
+  r[5] = (a[2] * a[3] - a[0] * a[5]) * id;
+  r[6] = (a[3] * a[7] - a[4] * a[6]) * id;
+  r[7] = (a[1] * a[6] - a[0] * a[7]) * id;
+  r[8] = (a[0] * a[4] - a[1] * a[3]) * id;
+  return 1;
+}
+
+/* Procrustes: R, t minimising sum ||R pw + t - pc||^2 (Kabsch). */
+static void procrustes(const double* pw, const double* pc, int n, double* R, double* t) {
+  double cw[3] = {0, 0, 0}, cc[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 3; ++j) { cw[j] += pw[3 * i + j]; cc[j] += pc[3 * i + j]; }
+  for (int j = 0; j < 3; ++j) { cw[j] /= n; cc[j] /= n; }
+  double H[9] = {0}; /* H = sum (pc - cc)(pw - cw)^T   (ABt in EPnP) */
+  for (int i = 0; i < n; ++i)
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) H[r * 3 + c] += (pc[3 * i + r] - cc[r]) * (pw[3 * i + c] - cw[c]);
+  /* SVD H = U S V^T through eig(H^T H) = V S^2 V^T, U = H V / S */
+  double HtH[9], w[3], V[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0;
+      for (int k = 0; k < 3; ++k) s += H[k * 3 + i] * H[k * 3 + j];
+      HtH[i * 3 + j] = s;
+    }
+  jacobi_eig(HtH, 3, w, V); /* rows of V = right singular vectors */
+  double U[9];
+  for (int i = 0; i < 2; ++i) {
+    double u[3];
+    for (int r = 0; r < 3; ++r) u[r] = H[r * 3 + 0] * V[i * 3 + 0] + H[r * 3 + 1] * V[i * 3 + 1] + H[r * 3 + 2] * V[i * 3 + 2];
+    double nr = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    if (nr < 1e-300) nr = 1e-300;
+    for (int r = 0; r < 3; ++r) U[i * 3 + r] = u[r] / nr; /* U stored by rows = left vectors */
+  }
+  /* re-orthogonalise u1 against u0 */
+  {
+    double d = U[0] * U[3] + U[1] * U[4] + U[2] * U[5];
+    for (int r = 0; r < 3; ++r) U[3 + r] -= d * U[r];
+    double nr = sqrt(U[3] * U[3] + U[4] * U[4] + U[5] * U[5]);
+    if (nr < 1e-300) nr = 1e-300;
+    for (int r = 0; r < 3; ++r) U[3 + r] /= nr;
+  }
+  U[6] = U[1] * U[5] - U[2] * U[4];
+  U[7] = U[2] * U[3] - U[0] * U[5];
+  U[8] = U[0] * U[4] - U[1] * U[3];
+  /* third right vector consistent with det(V) = +1 */
+  double v2[3] = {V[1] * V[5] - V[2] * V[4], V[2] * V[3] - V[0] * V[5], V[0] * V[4] - V[1] * V[3]};
+  /* R = sum_i u_i v_i^T (u2 = u0 x u1, v2 = v0 x v1 gives det(R) = +1: Kabsch) */
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      R[r * 3 + c] = U[0 * 3 + r] * V[0 * 3 + c] + U[1 * 3 + r] * V[1 * 3 + c] + U[2 * 3 + r] * v2[c];
+  for (int r = 0; r < 3; ++r) t[r] = cc[r] - (R[r * 3 + 0] * cw[0] + R[r * 3 + 1] * cw[1] + R[r * 3 + 2] * cw[2]);
+}
+
+/* ---------------- EPnP ---------------- */
+
+typedef struct {
+  double fu, fv, uc, vc;
+} Cam;
+
+static void ctrl_points(const double* pw, int n, double cws[4][3], double ccinv[9]) {
+  double c0[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 3; ++j) c0[j] += pw[3 * i + j];
+  for (int j = 0; j < 3; ++j) c0[j] /= n;
+  double C[9] = {0};
+  for (int i = 0; i < n; ++i)
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) C[r * 3 + c] += (pw[3 * i + r] - c0[r]) * (pw[3 * i + c] - c0[c]);
+  double w[3], V[9];
+  jacobi_eig(C, 3, w, V);
+  for (int j = 0; j < 3; ++j) cws[0][j] = c0[j];
+  for (int i = 0; i < 3; ++i) {
+    const double k = sqrt((w[i] > 0 ? w[i] : 0.0) / n);
+    for (int j = 0; j < 3; ++j) cws[i + 1][j] = c0[j] + k * V[i * 3 + j];
+  }
+  double CC[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 1; j < 4; ++j) CC[i * 3 + j - 1] = cws[j][i] - cws[0][i];
+  if (!inv3(CC, ccinv)) memset(ccinv, 0, sizeof(double) * 9);
+}
+
+static void alphas_of(const double* p, double cws[4][3], const double* ci, double a[4]) {
+  const double d0 = p[0] - cws[0][0], d1 = p[1] - cws[0][1], d2 = p[2] - cws[0][2];
+  a[1] = ci[0] * d0 + ci[1] * d1 + ci[2] * d2;
+  a[2] = ci[3] * d0 + ci[4] * d1 + ci[5] * d2;
+  a[3] = ci[6] * d0 + ci[7] * d1 + ci[8] * d2;
+  a[0] = 1.0 - a[1] - a[2] - a[3];
+}
+
+static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+static void gauss_newton(const double* L, const double* rho, double betas[4]) {
+  for (int it = 0; it < 5; ++it) {
+    double A[24], b[6], x[4];
+    for (int i = 0; i < 6; ++i) {
+      const double* l = L + 10 * i;
+      double* a = A + 4 * i;
+      a[0] = 2 * l[0] * betas[0] + l[1] * betas[1] + l[3] * betas[2] + l[6] * betas[3];
+      a[1] = l[1] * betas[0] + 2 * l[2] * betas[1] + l[4] * betas[2] + l[7] * betas[3];
+      a[2] = l[3] * betas[0] + l[4] * betas[1] + 2 * l[5] * betas[2] + l[8] * betas[3];
+      a[3] = l[6] * betas[0] + l[7] * betas[1] + l[8] * betas[2] + 2 * l[9] * betas[3];
+      b[i] = rho[i] - (l[0] * betas[0] * betas[0] + l[1] * betas[0] * betas[1] + l[2] * betas[1] * betas[1] +
+                       l[3] * betas[0] * betas[2] + l[4] * betas[1] * betas[2] + l[5] * betas[2] * betas[2] +
+                       l[6] * betas[0] * betas[3] + l[7] * betas[1] * betas[3] + l[8] * betas[2] * betas[3] +
+                       l[9] * betas[3] * betas[3]);
+    }
+    lsq_solve(A, 6, 4, b, x);
+    for (int k = 0; k < 4; ++k) betas[k] += x[k];
+  }
+}
+
+/* R,t from betas; returns mean reprojection error */
+static double r_and_t(const double* ut, const double betas[4], const double* pw, const double* uv, int n,
+                      double cws[4][3], const double* ci, Cam cam, double* R, double* t, double* pcs_buf) {
+  double ccs[4][3] = {{0}};
+  for (int i = 0; i < 4; ++i) {
+    const double* v = ut + 12 * (11 - i);
+    for (int j = 0; j < 4; ++j)
+      for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[3 * j + k];
+  }
+  for (int p = 0; p < n; ++p) {
+    double a[4];
+    alphas_of(pw + 3 * p, cws, ci, a);
+    for (int k = 0; k < 3; ++k)
+      pcs_buf[3 * p + k] = a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k];
+  }
+  if (pcs_buf[2] < 0.0)
+    for (int p = 0; p < 3 * n; ++p) pcs_buf[p] = -pcs_buf[p];
+  procrustes(pw, pcs_buf, n, R, t);
+  double err = 0.0;
+  for (int p = 0; p < n; ++p) {
+    const double* X = pw + 3 * p;
+    const double Xc = dot3(R, X) + t[0], Yc = dot3(R + 3, X) + t[1], Zc = dot3(R + 6, X) + t[2];
+    const double iz = 1.0 / Zc;
+    const double ue = cam.uc + cam.fu * Xc * iz, ve = cam.vc + cam.fv * Yc * iz;
+    const double du = uv[2 * p] - ue, dv = uv[2 * p + 1] - ve;
+    err += sqrt(du * du + dv * dv);
+  }
+  return err / n;
+}
+
+static double pcs_scratch[3 * MAXP];
+
+/* EPnP on n >= 4 correspondences (pw: n x 3 world, uv: n x 2 pixels). */
+static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R, double* t) {
+  double cws[4][3], ci[9];
+  ctrl_points(pw, n, cws, ci);
+  double MtM[144] = {0};
+  for (int p = 0; p < n; ++p) {
+    double a[4];
+    alphas_of(pw + 3 * p, cws, ci, a);
+    double r1[12], r2[12];
+    for (int j = 0; j < 4; ++j) {
+      r1[3 * j] = a[j] * cam.fu;
+      r1[3 * j + 1] = 0.0;
+      r1[3 * j + 2] = a[j] * (cam.uc - uv[2 * p]);
+      r2[3 * j] = 0.0;
+      r2[3 * j + 1] = a[j] * cam.fv;
+      r2[3 * j + 2] = a[j] * (cam.vc - uv[2 * p + 1]);
+    }
+    for (int i = 0; i < 12; ++i)
+      for (int j = 0; j < 12; ++j) MtM[i * 12 + j] += r1[i] * r1[j] + r2[i] * r2[j];
+  }
+  double w[12], ut[144];
+  jacobi_eig(MtM, 12, w, ut);
+  /* L_6x10 and rho */
+  double L[60], rho[6];
+  {
+    const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+    double dv[4][6][3];
+    for (int i = 0; i < 4; ++i) {
+      int a = 0, b = 1;
+      for (int j = 0; j < 6; ++j) {
+        for (int k = 0; k < 3; ++k) dv[i][j][k] = v[i][3 * a + k] - v[i][3 * b + k];
+        if (++b > 3) { ++a; b = a + 1; }
+      }
+    }
+    for (int i = 0; i < 6; ++i) {
+      double* r = L + 10 * i;
+      r[0] = dot3(dv[0][i], dv[0][i]);
+      r[1] = 2.0 * dot3(dv[0][i], dv[1][i]);
+      r[2] = dot3(dv[1][i], dv[1][i]);
+      r[3] = 2.0 * dot3(dv[0][i], dv[2][i]);
+      r[4] = 2.0 * dot3(dv[1][i], dv[2][i]);
+      r[5] = dot3(dv[2][i], dv[2][i]);
+      r[6] = 2.0 * dot3(dv[0][i], dv[3][i]);
+      r[7] = 2.0 * dot3(dv[1][i], dv[3][i]);
+      r[8] = 2.0 * dot3(dv[2][i], dv[3][i]);
+      r[9] = dot3(dv[3][i], dv[3][i]);
+    }
+    int a = 0, b = 1;
+    for (int j = 0; j < 6; ++j) {
+      const double d0 = cws[a][0] - cws[b][0], d1 = cws[a][1] - cws[b][1], d2 = cws[a][2] - cws[b][2];
+      rho[j] = d0 * d0 + d1 * d1 + d2 * d2;
+      if (++b > 3) { ++a; b = a + 1; }
+    }
+  }
+  double Rs[4][9], ts[4][3], errs[4], betas[4];
+  /* approx 1: B11 B12 B13 B14 from columns 0 1 3 6 */
+  {
+    double A[24], x[4];
+    const int cols[4] = {0, 1, 3, 6};
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 4; ++j) A[4 * i + j] = L[10 * i + cols[j]];
+    lsq_solve(A, 6, 4, rho, x);
+    if (x[0] < 0) {
+      betas[0] = sqrt(-x[0]);
+      betas[1] = -x[1] / betas[0];
+      betas[2] = -x[2] / betas[0];
+      betas[3] = -x[3] / betas[0];
+    } else {
+      betas[0] = sqrt(x[0]);
+      betas[1] = betas[0] > 0 ? x[1] / betas[0] : 0.0;
+      betas[2] = betas[0] > 0 ? x[2] / betas[0] : 0.0;
+      betas[3] = betas[0] > 0 ? x[3] / betas[0] : 0.0;
+    }
+    gauss_newton(L, rho, betas);
+    errs[1] = r_and_t(ut, betas, pw, uv, n, cws, ci, cam, Rs[1], ts[1], pcs_scratch);
+  }
+  /* approx 2: B11 B12 B22 from columns 0 1 2 */
+  {
+    double A[18], x[3];
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 3; ++j) A[3 * i + j] = L[10 * i + j];
+    lsq_solve(A, 6, 3, rho, x);
+    if (x[0] < 0) {
+      betas[0] = sqrt(-x[0]);
+      betas[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
+    } else {
+      betas[0] = sqrt(x[0]);
+      betas[1] = (x[2] > 0) ? sqrt(x[2]) : 0.0;
+    }
+    if (x[1] < 0) betas[0] = -betas[0];
+    betas[2] = 0.0;
+    betas[3] = 0.0;
+    gauss_newton(L, rho, betas);
+    errs[2] = r_and_t(ut, betas, pw, uv, n, cws, ci, cam, Rs[2], ts[2], pcs_scratch);
+  }
+  /* approx 3: B11 B12 B22 B13 B23 from columns 0..4 */
+  {
+    double A[30], x[5];
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 5; ++j) A[5 * i + j] = L[10 * i + j];
+    lsq_solve(A, 6, 5, rho, x);
+    if (x[0] < 0) {
+      betas[0] = sqrt(-x[0]);
+      betas[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
+    } else {
+      betas[0] = sqrt(x[0]);
+      betas[1] = (x[2] > 0) ? sqrt(x[2]) : 0.0;
+    }
+    if (x[1] < 0) betas[0] = -betas[0];
+    betas[2] = betas[0] != 0.0 ? x[3] / betas[0] : 0.0;
+    betas[3] = 0.0;
+    gauss_newton(L, rho, betas);
+    errs[3] = r_and_t(ut, betas, pw, uv, n, cws, ci, cam, Rs[3], ts[3], pcs_scratch);
+  }
+  int N = 1;
+  if (errs[2] < errs[1]) N = 2;
+  if (errs[3] < errs[N]) N = 3;
+  memcpy(R, Rs[N], sizeof(double) * 9);
+  memcpy(t, ts[N], sizeof(double) * 3);
+  return errs[N];
+}
+
+/* ---------------- public oracle entry points ---------------- */
+
+/* EPnP on the given points (double). Returns mean reprojection error. */
+double oracle_epnp(const double* pw, const double* uv, int n, const double* K4, double* R, double* t) {
+  Cam cam = {K4[0], K4[1], K4[2], K4[3]};
+  return epnp(pw, uv, n, cam, R, t);
+}
+
+/*
+ * RANSAC with caller-given hypothesis subsets.
+ * obj: P x 3 (f32, metres, model frame), img: P x 2 (f32, pixels), K4 = fx, fy, cx, cy.
+ * subsets: H x 5 indices into [0, P). thr: reprojection threshold in pixels.
+ * Outputs R (9, f32 row-major), t (3), inlier mask (P bytes) of the final pose's source
+ * hypothesis, and returns the inlier count of the best hypothesis (0 = RANSAC failed).
+ */
+int oracle_pnp_ransac(const float* obj, const float* img, int P, const float* K4, const int* subsets, int H,
+                      float thr, float* R_out, float* t_out, unsigned char* inlier_mask, int* best_h) {
+  static double pw[3 * MAXP], uv[2 * MAXP];
+  Cam cam = {K4[0], K4[1], K4[2], K4[3]};
+  if (P > MAXP) P = MAXP;
+  int best = -1, best_cnt = 0;
+  double bestR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, bestt[3] = {0, 0, 0};
+  const float thr2 = thr * thr;
+  for (int h = 0; h < H; ++h) {
+    double spw[15], suv[10], R[9], t[3];
+    for (int i = 0; i < 5; ++i) {
+      const int id = subsets[5 * h + i];
+      for (int k = 0; k < 3; ++k) spw[3 * i + k] = obj[3 * id + k];
+      for (int k = 0; k < 2; ++k) suv[2 * i + k] = img[2 * id + k];
+    }
+    epnp(spw, suv, 5, cam, R, t);
+    int cnt = 0;
+    for (int p = 0; p < P; ++p) {
+      const float X = obj[3 * p], Y = obj[3 * p + 1], Z = obj[3 * p + 2];
+      const float xc = (float)R[0] * X + (float)R[1] * Y + (float)R[2] * Z + (float)t[0];
+      const float yc = (float)R[3] * X + (float)R[4] * Y + (float)R[5] * Z + (float)t[1];
+      const float zc = (float)R[6] * X + (float)R[7] * Y + (float)R[8] * Z + (float)t[2];
+      const float iz = 1.0f / zc;
+      const float du = img[2 * p] - ((float)cam.fu * xc * iz + (float)cam.uc);
+      const float dv = img[2 * p + 1] - ((float)cam.fv * yc * iz + (float)cam.vc);
+      if (du * du + dv * dv <= thr2) ++cnt;
+    }
+    if (cnt > (best_cnt > 4 ? best_cnt : 4)) {
+      best_cnt = cnt;
+      best = h;
+      memcpy(bestR, R, sizeof bestR);
+      memcpy(bestt, t, sizeof bestt);
+    }
+  }
+  if (best_h) *best_h = best;
+  double R[9], t[3];
+  memcpy(R, bestR, sizeof R);
+  memcpy(t, bestt, sizeof t);
+  int n = 0;
+  for (int p = 0; p < P; ++p) {
+    int in = 0;
+    if (best >= 0) {
+      const float X = obj[3 * p], Y = obj[3 * p + 1], Z = obj[3 * p + 2];
+      const float xc = (float)bestR[0] * X + (float)bestR[1] * Y + (float)bestR[2] * Z + (float)bestt[0];
+      const float yc = (float)bestR[3] * X + (float)bestR[4] * Y + (float)bestR[5] * Z + (float)bestt[1];
+      const float zc = (float)bestR[6] * X + (float)bestR[7] * Y + (float)bestR[8] * Z + (float)bestt[2];
+      const float iz = 1.0f / zc;
+      const float du = img[2 * p] - ((float)cam.fu * xc * iz + (float)cam.uc);
+      const float dv = img[2 * p + 1] - ((float)cam.fv * yc * iz + (float)cam.vc);
+      in = du * du + dv * dv <= thr2;
+    }
+    if (inlier_mask) inlier_mask[p] = (unsigned char)in;
+    if (in) {
+      for (int k = 0; k < 3; ++k) pw[3 * n + k] = obj[3 * p + k];
+      for (int k = 0; k < 2; ++k) uv[2 * n + k] = img[2 * p + k];
+      ++n;
+    }
+  }
+  if (best >= 0 && n >= 5) epnp(pw, uv, n, cam, R, t);
+  for (int i = 0; i < 9; ++i) R_out[i] = (float)R[i];
+  for (int i = 0; i < 3; ++i) t_out[i] = (float)t[i];
+  return best >= 0 ? best_cnt : 0;
+}

@@ -1,0 +1,290 @@
+// 3D-GCN fusion kernels (FusionNetLite, lib/network/point/fusion.py:137-240).
+//
+//   krrn_knn_f32        get_neighbor_index / get_nearest_index (gcn3d.py:15-38) without the
+//                       [n, n] distance matrix: candidates staged through LDS, top-(k+1) kept
+//                       in registers, ties broken towards the lower index (the documented rule;
+//                       torch.topk leaves tie order unspecified).
+//   krrn_gcn_conv_f32   Conv_surface (gcn3d.py:88-112) and the gather/theta/max/sum half of
+//                       Conv_layer / Conv_fuse_layer (gcn3d.py:136-216) fused with the BN1d +
+//                       ReLU that FusionNetLite applies (fusion.py:183-213). The
+//                       [n, k, S*C] theta / gathered / product tensors of the reference
+//                       never exist: each neighbour row of the GEMM output Y is read once
+//                       per (support, channel) straight from L2.
+//   krrn_pool_max_f32   Pool_layer's max over the 4 neighbours (gcn3d.py:233-236), evaluated
+//                       only at the randperm-sampled rows that the reference keeps (:238-241).
+#include <math.h>
+
+#include "krrn_common.h"
+
+namespace {
+
+constexpr int kKnnThreads = 256;
+constexpr int kKnnChunk = 1024;  // candidates per LDS stage
+constexpr int kKnnKmax = 16;
+
+// Exact, FMA-free f32 expression order (documented in DESIGN.md / oracle/krrn_oracle.py):
+//   inner = ((q0*c0 + q1*c1) + q2*c2) ...   (sequential over d, every op rounded)
+//   |p|^2 = ((p0*p0 + p1*p1) + p2*p2) ...
+//   neighbor (gcn3d.py:23): dist = ((inner * -2) + |c|^2) + |q|^2
+//   nearest  (gcn3d.py:36): dist = (|c|^2 + |q|^2) - 2 * inner
+template <int D>
+__device__ __forceinline__ float knn_sqnorm(const float* p) {
+#pragma clang fp contract(off)
+  float s = p[0] * p[0];
+#pragma unroll
+  for (int i = 1; i < D; ++i) s = s + p[i] * p[i];
+  return s;
+}
+
+template <int D>
+__device__ __forceinline__ float knn_inner(const float* a, const float* b) {
+#pragma clang fp contract(off)
+  float s = a[0] * b[0];
+#pragma unroll
+  for (int i = 1; i < D; ++i) s = s + a[i] * b[i];
+  return s;
+}
+
+template <int D>
+__global__ __launch_bounds__(kKnnThreads) void knn_kernel(
+    const float* __restrict__ q, long long q_bs, int q_st, int nq, const int* __restrict__ qidx,
+    const float* __restrict__ c, long long c_bs, int c_st, int nc, int K, int drop, int mode,
+    int* __restrict__ out) {
+#pragma clang fp contract(off)
+  constexpr int DP = D == 3 ? 4 : 12;  // LDS record: coords + |c|^2 (+ pad)
+  __shared__ __attribute__((aligned(16))) float sc[kKnnChunk * DP];
+  const int b = blockIdx.y;
+  const int t = blockIdx.x * kKnnThreads + threadIdx.x;
+  const bool active = t < nq;
+  float qp[D];
+  float qn = 0.f;
+  if (active) {
+    const int qi = qidx ? qidx[t] : t;
+    const float* src = q + b * q_bs + (long long)qi * q_st;
+#pragma unroll
+    for (int i = 0; i < D; ++i) qp[i] = src[i];
+    qn = knn_sqnorm<D>(qp);
+  } else {
+#pragma unroll
+    for (int i = 0; i < D; ++i) qp[i] = 0.f;
+  }
+  float bd[kKnnKmax];
+  int bi[kKnnKmax];
+#pragma unroll
+  for (int i = 0; i < kKnnKmax; ++i) { bd[i] = INFINITY; bi[i] = 0x7fffffff; }
+  float thr = INFINITY;
+
+  const float* cb = c + b * c_bs;
+  for (int j0 = 0; j0 < nc; j0 += kKnnChunk) {
+    const int cnt = min(kKnnChunk, nc - j0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < cnt; j += kKnnThreads) {
+      const float* src = cb + (long long)(j0 + j) * c_st;
+      float p[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) p[i] = src[i];
+      float* dst = sc + j * DP;
+#pragma unroll
+      for (int i = 0; i < D; ++i) dst[i] = p[i];
+      dst[D] = knn_sqnorm<D>(p);
+    }
+    __syncthreads();
+    if (active) {
+      for (int j = 0; j < cnt; ++j) {
+        const float* p = sc + j * DP;
+        const float inner = knn_inner<D>(qp, p);
+        const float cn = p[D];
+        const float d = mode == 0 ? ((inner * -2.f) + cn) + qn : (cn + qn) - 2.f * inner;
+        if (d < thr) {
+          // branch-free insertion into the ascending list; strict '<' keeps the earlier
+          // (lower) index first among equal distances. Slots >= K are scratch.
+          float nd = d;
+          int ni = j0 + j;
+#pragma unroll
+          for (int s = 0; s < kKnnKmax; ++s) {
+            const bool sw = nd < bd[s];
+            const float td = bd[s];
+            const int ti = bi[s];
+            bd[s] = sw ? nd : td;
+            bi[s] = sw ? ni : ti;
+            nd = sw ? td : nd;
+            ni = sw ? ti : ni;
+          }
+          float tv = INFINITY;
+#pragma unroll
+          for (int s = 0; s < kKnnKmax; ++s) tv = (s == K - 1) ? bd[s] : tv;
+          thr = tv;
+        }
+      }
+    }
+  }
+  if (active) {
+    const int ko = K - drop;
+    int* o = out + ((long long)b * nq + t) * ko;
+#pragma unroll
+    for (int s = 0; s < kKnnKmax; ++s)
+      if (s >= drop && s < K) o[s - drop] = bi[s];
+  }
+}
+
+}  // namespace
+
+KRRN_API int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, const int* qidx, const float* c,
+                          long long c_bs, int c_st, int nc, int d, int k, int drop_first, int mode, int B,
+                          int* out, void* stream) {
+  if (!q || !c || !out) return KRRN_EARG;
+  if (d != 3 && d != 9) return KRRN_ESHAPE;
+  if (k < 1 || k + (drop_first ? 1 : 0) > kKnnKmax || nq < 1 || nc < 1 || B < 1) return KRRN_ESHAPE;
+  if (k + (drop_first ? 1 : 0) > nc) return KRRN_ESHAPE;
+  if (mode != 0 && mode != 1) return KRRN_EARG;
+  const int K = k + (drop_first ? 1 : 0);
+  dim3 grid(krrn_cdiv(nq, kKnnThreads), B);
+  hipStream_t s = (hipStream_t)stream;
+  if (d == 3)
+    hipLaunchKernelGGL(knn_kernel<3>, grid, dim3(kKnnThreads), 0, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc,
+                       K, drop_first ? 1 : 0, mode, out);
+  else
+    hipLaunchKernelGGL(knn_kernel<9>, grid, dim3(kKnnThreads), 0, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc,
+                       K, drop_first ? 1 : 0, mode, out);
+  return krrn_launch_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// GCN gather-conv
+// ------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kGcnThreads = 128;
+constexpr int kGcnPts = 8;  // points per block
+constexpr int kGcnKmax = 16;
+
+template <int D, bool HAS_Y>
+__global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
+    const int* __restrict__ idx, int n, int k, const float* __restrict__ v, long long v_bs, int v_st,
+    const float* __restrict__ dn, int S, int C, const float* __restrict__ Y,
+    const float* __restrict__ bn_s, const float* __restrict__ bn_b, int relu, float* __restrict__ out,
+    long long o_bs, int o_st) {
+  __shared__ float sdir[kGcnPts * kGcnKmax * D];
+  __shared__ int snb[kGcnPts * kGcnKmax];
+  const int b = blockIdx.y;
+  const int p0 = blockIdx.x * kGcnPts;
+  const int np = min(kGcnPts, n - p0);
+  const float* vb = v + b * v_bs;
+  // 1) neighbour directions, F.normalize(v[j] - v[i], dim=-1) (gcn3d.py:60-69)
+  for (int e = threadIdx.x; e < np * k; e += kGcnThreads) {
+    const int p = e / k, j = e - (e / k) * k;
+    const int pi = p0 + p;
+    const int nj = idx[((long long)b * n + pi) * k + j];
+    snb[p * kGcnKmax + j] = nj;
+    float dv[D];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      dv[i] = vb[(long long)nj * v_st + i] - vb[(long long)pi * v_st + i];
+      ss += dv[i] * dv[i];
+    }
+    const float nr = fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+    for (int i = 0; i < D; ++i) sdir[(p * kGcnKmax + j) * D + i] = dv[i] / nr;
+  }
+  __syncthreads();
+  const int SC = S * C;
+  const long long yrow = (long long)(S + 1) * C;
+  const float* yb = HAS_Y ? Y + b * (long long)n * yrow : nullptr;
+  for (int c = threadIdx.x; c < C; c += kGcnThreads) {
+    float acc[kGcnPts];
+#pragma unroll
+    for (int p = 0; p < kGcnPts; ++p) acc[p] = 0.f;
+    for (int s = 0; s < S; ++s) {
+      float w[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) w[i] = dn[(long long)i * SC + s * C + c];
+#pragma unroll
+      for (int p = 0; p < kGcnPts; ++p) {
+        if (p < np) {
+          float m = -INFINITY;
+          for (int j = 0; j < k; ++j) {
+            const float* dr = sdir + (p * kGcnKmax + j) * D;
+            float th = 0.f;
+#pragma unroll
+            for (int i = 0; i < D; ++i) th += dr[i] * w[i];
+            th = fmaxf(th, 0.f);
+            float val = th;
+            if constexpr (HAS_Y) val = th * yb[(long long)snb[p * kGcnKmax + j] * yrow + C + s * C + c];
+            m = fmaxf(m, val);
+          }
+          acc[p] += m;
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kGcnPts; ++p) {
+      if (p < np) {
+        float o = acc[p];
+        if constexpr (HAS_Y) o = yb[(long long)(p0 + p) * yrow + c] + o;
+        if (bn_s) o = o * bn_s[c] + bn_b[c];
+        if (relu) o = fmaxf(o, 0.f);
+        out[b * o_bs + (long long)(p0 + p) * o_st + c] = o;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, long long v_bs, int v_st, int d,
+                               const float* dn, int S, int C, const float* Y, const float* bn_scale,
+                               const float* bn_bias, int relu, float* out, long long o_bs, int o_st, int B,
+                               void* stream) {
+  if (!idx || !v || !dn || !out) return KRRN_EARG;
+  if ((bn_scale == nullptr) != (bn_bias == nullptr)) return KRRN_EARG;
+  if (d != 3 && d != 9) return KRRN_ESHAPE;
+  if (k < 1 || k > kGcnKmax || n < 1 || S < 1 || C < 1 || B < 1) return KRRN_ESHAPE;
+  dim3 grid(krrn_cdiv(n, kGcnPts), B);
+  hipStream_t s = (hipStream_t)stream;
+#define KRRN_GCN_LAUNCH(DD, HY)                                                                         \
+  hipLaunchKernelGGL((gcn_conv_kernel<DD, HY>), grid, dim3(kGcnThreads), 0, s, idx, n, k, v, v_bs, v_st, dn, \
+                     S, C, Y, bn_scale, bn_bias, relu, out, o_bs, o_st)
+  if (d == 3) {
+    if (Y) KRRN_GCN_LAUNCH(3, true); else KRRN_GCN_LAUNCH(3, false);
+  } else {
+    if (Y) KRRN_GCN_LAUNCH(9, true); else KRRN_GCN_LAUNCH(9, false);
+  }
+#undef KRRN_GCN_LAUNCH
+  return krrn_launch_status();
+}
+
+// ------------------------------------------------------------------------------------------
+// Pool_layer max at the sampled rows
+// ------------------------------------------------------------------------------------------
+namespace {
+__global__ void pool_max_kernel(const int* __restrict__ nbr, int nq, int kk, const float* __restrict__ F,
+                                long long f_bs, int f_st, int C4, float* __restrict__ out, long long o_bs,
+                                int o_st) {
+  const int b = blockIdx.y;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)nq * C4) return;
+  const int t = (int)(e / C4), c4 = (int)(e - (e / C4) * C4);
+  const int* nb = nbr + ((long long)b * nq + t) * kk;
+  const float* fb = F + b * f_bs;
+  f32x4 m = *reinterpret_cast<const f32x4*>(fb + (long long)nb[0] * f_st + 4 * c4);
+  for (int j = 1; j < kk; ++j) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(fb + (long long)nb[j] * f_st + 4 * c4);
+    m.x = fmaxf(m.x, x.x); m.y = fmaxf(m.y, x.y); m.z = fmaxf(m.z, x.z); m.w = fmaxf(m.w, x.w);
+  }
+  *reinterpret_cast<f32x4*>(out + b * o_bs + (long long)t * o_st + 4 * c4) = m;
+}
+}  // namespace
+
+KRRN_API int krrn_pool_max_f32(const int* nbr, int nq, int kk, const float* F, long long f_bs, int f_st, int C,
+                               float* out, long long o_bs, int o_st, int B, void* stream) {
+  if (!nbr || !F || !out) return KRRN_EARG;
+  if (nq < 1 || kk < 1 || C < 1 || B < 1) return KRRN_ESHAPE;
+  if ((C & 3) || (f_st & 3) || (o_st & 3) || (f_bs & 3) || (o_bs & 3) || !krrn_aligned16(F) || !krrn_aligned16(out))
+    return KRRN_EALIGN;
+  const long long tot = (long long)nq * (C / 4);
+  dim3 grid((unsigned)((tot + 255) / 256), B);
+  hipLaunchKernelGGL(pool_max_kernel, grid, dim3(256), 0, (hipStream_t)stream, nbr, nq, kk, F, f_bs, f_st, C / 4,
+                     out, o_bs, o_st);
+  return krrn_launch_status();
+}

@@ -1,0 +1,304 @@
+// Memory-bound glue of the KRRN forward: bilinear resampling (HRNet fuse / final concat,
+// myhrnet.py:242-245, 511-516; UpsamplingBilinear2d in the heads, krrn.py:56, 78), layout
+// changes at the API boundary, class selection + normal normalisation (krrn.py:100-108),
+// the `choose` gather (krrn.py:121-122), row gathers (Pool_layer sampling, the final
+// concat of fusion.py:234-238, the one-hot column of krrn.py:132-138) and the TBase tail
+// (posenet.py:76-80 + krrn.py:153).
+#include <math.h>
+
+#include "krrn_common.h"
+
+namespace {
+
+// PyTorch's upsample_bilinear2d source index (aten/src/ATen/native/UpSample.h,
+// area_pixel_compute_source_index) evaluated in f32.
+__device__ __forceinline__ void src_index(int dst, int in_size, float scale, int align, int& i0, int& i1,
+                                          float& l0, float& l1) {
+  float s;
+  if (align) {
+    s = scale * (float)dst;
+  } else {
+    s = scale * ((float)dst + 0.5f) - 0.5f;
+    s = s < 0.f ? 0.f : s;
+  }
+  int i = (int)s;
+  i = i > in_size - 1 ? in_size - 1 : i;
+  i0 = i;
+  i1 = i + ((i < in_size - 1) ? 1 : 0);
+  float lam = s - (float)i;
+  lam = fminf(fmaxf(lam, 0.f), 1.f);
+  l1 = lam;
+  l0 = 1.f - lam;
+}
+
+__global__ void resize_bilinear_kernel(const float* __restrict__ in, int Hi, int Wi, int in_cs, int in_co, int C4,
+                                       float* __restrict__ out, int Ho, int Wo, int out_cs, int out_co,
+                                       const float* __restrict__ add, int add_cs, int add_co, float sh, float sw,
+                                       int align, int relu, long long total) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c4 = (int)(e % C4);
+  long long p = e / C4;
+  const int ox = (int)(p % Wo);
+  p /= Wo;
+  const int oy = (int)(p % Ho);
+  const int b = (int)(p / Ho);
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  src_index(oy, Hi, sh, align, y0, y1, ly0, ly1);
+  src_index(ox, Wi, sw, align, x0, x1, lx0, lx1);
+  const float* ib = in + (long long)b * Hi * Wi * in_cs + in_co + 4 * c4;
+  const f32x4 v00 = *reinterpret_cast<const f32x4*>(ib + ((long long)y0 * Wi + x0) * in_cs);
+  const f32x4 v01 = *reinterpret_cast<const f32x4*>(ib + ((long long)y0 * Wi + x1) * in_cs);
+  const f32x4 v10 = *reinterpret_cast<const f32x4*>(ib + ((long long)y1 * Wi + x0) * in_cs);
+  const f32x4 v11 = *reinterpret_cast<const f32x4*>(ib + ((long long)y1 * Wi + x1) * in_cs);
+  f32x4 r = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+  const long long opix = ((long long)b * Ho + oy) * Wo + ox;
+  if (add) r = *reinterpret_cast<const f32x4*>(add + opix * add_cs + add_co + 4 * c4) + r;
+  if (relu) {
+    r.x = fmaxf(r.x, 0.f); r.y = fmaxf(r.y, 0.f); r.z = fmaxf(r.z, 0.f); r.w = fmaxf(r.w, 0.f);
+  }
+  *reinterpret_cast<f32x4*>(out + opix * out_cs + out_co + 4 * c4) = r;
+}
+
+__global__ void add_relu_kernel(const float* __restrict__ a, int a_cs, int a_co, const float* __restrict__ b,
+                                int b_cs, int b_co, float* __restrict__ out, int o_cs, int o_co, int C4, int relu,
+                                long long total) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c4 = (int)(e % C4);
+  const long long pix = e / C4;
+  f32x4 r = *reinterpret_cast<const f32x4*>(a + pix * a_cs + a_co + 4 * c4);
+  if (b) r = r + *reinterpret_cast<const f32x4*>(b + pix * b_cs + b_co + 4 * c4);
+  if (relu) {
+    r.x = fmaxf(r.x, 0.f); r.y = fmaxf(r.y, 0.f); r.z = fmaxf(r.z, 0.f); r.w = fmaxf(r.w, 0.f);
+  }
+  *reinterpret_cast<f32x4*>(out + pix * o_cs + o_co + 4 * c4) = r;
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, int C, int HW, float* __restrict__ out, int o_cs,
+                                    int o_co, long long total) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int p = (int)(e % HW);
+  const long long bc = e / HW;
+  const int c = (int)(bc % C);
+  const long long b = bc / C;
+  out[(b * HW + p) * o_cs + o_co + c] = in[e];
+}
+
+__global__ void heads_select_kernel(const float* __restrict__ fx, int Cx, int xyz_off, const float* __restrict__ fn,
+                                    int Cn, const long long* __restrict__ cls, float* __restrict__ xyz,
+                                    float* __restrict__ nml, int HW, long long total) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int p = (int)(e % HW);
+  const long long b = e / HW;
+  const int c = (int)cls[b];
+  const float* sx = fx + (b * Cx + xyz_off + 3 * c) * HW + p;
+  const float* sn = fn + (b * Cn + 3 * c) * HW + p;
+  float* dx = xyz + b * 3 * HW + p;
+  float* dn = nml + b * 3 * HW + p;
+  dx[0] = sx[0];
+  dx[HW] = sx[HW];
+  dx[2 * HW] = sx[2 * HW];
+  const float n0 = sn[0], n1 = sn[HW], n2 = sn[2 * HW];
+  // F.normalize(p=2, dim=1, eps=1e-12): x / max(||x||_2, eps)
+  const float nr = fmaxf(sqrtf(n0 * n0 + n1 * n1 + n2 * n2), 1e-12f);
+  dn[0] = n0 / nr;
+  dn[HW] = n1 / nr;
+  dn[2 * HW] = n2 / nr;
+}
+
+__global__ void points_gather_kernel(const float* __restrict__ cloud, const float* __restrict__ xyz,
+                                     const float* __restrict__ nml, const long long* __restrict__ choose, int N,
+                                     int HW, float* __restrict__ p9, long long total) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const long long b = e / N;
+  const long long pix = choose[e];
+  float* o = p9 + e * 9;
+  const float* cl = cloud + e * 3;
+  o[0] = cl[0];
+  o[1] = cl[1];
+  o[2] = cl[2];
+  const float* x = xyz + b * 3 * HW + pix;
+  const float* n = nml + b * 3 * HW + pix;
+  o[3] = x[0];
+  o[4] = x[HW];
+  o[5] = x[2 * HW];
+  o[6] = n[0];
+  o[7] = n[HW];
+  o[8] = n[2 * HW];
+}
+
+template <bool IDX64, bool VEC>
+__global__ void gather_rows_kernel(const void* __restrict__ idx, long long idx_bs, int nrows,
+                                   const float* __restrict__ src, long long src_bs, int src_st,
+                                   float* __restrict__ dst, long long dst_bs, int dst_st, int width,
+                                   long long total) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int wq = VEC ? width / 4 : width;
+  const int w = (int)(e % wq);
+  const long long br = e / wq;
+  const int r = (int)(br % nrows);
+  const long long b = br / nrows;
+  const long long ii = b * idx_bs + r;
+  const long long row = IDX64 ? ((const long long*)idx)[ii] : (long long)((const int*)idx)[ii];
+  const float* s = src + b * src_bs + row * src_st;
+  float* d = dst + b * dst_bs + (long long)r * dst_st;
+  if constexpr (VEC) {
+    *reinterpret_cast<f32x4*>(d + 4 * w) = *reinterpret_cast<const f32x4*>(s + 4 * w);
+  } else {
+    d[w] = s[w];
+  }
+}
+
+// pred_t[b] = mean_i( cloud[b, i] + W4[0:3] . h[b, i] + b4[0:3] )   (one block per crop)
+__global__ __launch_bounds__(256) void tbase_tail_kernel(const float* __restrict__ h, int n, int C,
+                                                         const float* __restrict__ w4,
+                                                         const float* __restrict__ b4,
+                                                         const float* __restrict__ cloud,
+                                                         float* __restrict__ pred_t, float* __restrict__ t_res) {
+  __shared__ float red[4][3];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float sx = 0.f, sy = 0.f, sz = 0.f;
+  for (int i = wave; i < n; i += 4) {
+    const float* hr = h + ((long long)b * n + i) * C;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float x = hr[c];
+      a0 += w4[c] * x;
+      a1 += w4[C + c] * x;
+      a2 += w4[2 * C + c] * x;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      a0 += __shfl_xor(a0, off);
+      a1 += __shfl_xor(a1, off);
+      a2 += __shfl_xor(a2, off);
+    }
+    const float t0 = a0 + b4[0], t1 = a1 + b4[1], t2 = a2 + b4[2];
+    const float* cp = cloud + ((long long)b * n + i) * 3;
+    if (lane == 0) {
+      if (t_res) {
+        float* tr = t_res + ((long long)b * n + i) * 3;
+        tr[0] = t0; tr[1] = t1; tr[2] = t2;
+      }
+      sx += cp[0] + t0;
+      sy += cp[1] + t1;
+      sz += cp[2] + t2;
+    }
+  }
+  if (lane == 0) {
+    red[wave][0] = sx; red[wave][1] = sy; red[wave][2] = sz;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int j = threadIdx.x;
+    pred_t[b * 3 + j] = (red[0][j] + red[1][j] + red[2][j] + red[3][j]) / (float)n;
+  }
+}
+
+inline dim3 grid1(long long total) { return dim3((unsigned)((total + 255) / 256)); }
+
+}  // namespace
+
+KRRN_API int krrn_resize_bilinear_f32(const float* in, int B, int Hi, int Wi, int in_cs, int in_co, int C,
+                                      float* out, int Ho, int Wo, int out_cs, int out_co, const float* add,
+                                      int add_cs, int add_co, int align_corners, int relu, void* stream) {
+  if (!in || !out) return KRRN_EARG;
+  if (B < 1 || Hi < 1 || Wi < 1 || Ho < 1 || Wo < 1 || C < 1) return KRRN_ESHAPE;
+  if ((C & 3) || (in_cs & 3) || (in_co & 3) || (out_cs & 3) || (out_co & 3) || !krrn_aligned16(in) ||
+      !krrn_aligned16(out))
+    return KRRN_EALIGN;
+  if (add && ((add_cs & 3) || (add_co & 3) || !krrn_aligned16(add))) return KRRN_EALIGN;
+  float sh, sw;
+  if (align_corners) {
+    sh = Ho > 1 ? (float)(Hi - 1) / (float)(Ho - 1) : 0.f;
+    sw = Wo > 1 ? (float)(Wi - 1) / (float)(Wo - 1) : 0.f;
+  } else {
+    sh = (float)Hi / (float)Ho;
+    sw = (float)Wi / (float)Wo;
+  }
+  const long long total = (long long)B * Ho * Wo * (C / 4);
+  hipLaunchKernelGGL(resize_bilinear_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, in, Hi, Wi, in_cs,
+                     in_co, C / 4, out, Ho, Wo, out_cs, out_co, add, add_cs, add_co, sh, sw, align_corners, relu,
+                     total);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_add_relu_f32(const float* a, int a_cs, int a_co, const float* b, int b_cs, int b_co, float* out,
+                               int o_cs, int o_co, long long npix, int C, int relu, void* stream) {
+  if (!a || !out) return KRRN_EARG;
+  if (npix < 1 || C < 1) return KRRN_ESHAPE;
+  if ((C & 3) || (a_cs & 3) || (a_co & 3) || (o_cs & 3) || (o_co & 3) || (b && ((b_cs & 3) || (b_co & 3))))
+    return KRRN_EALIGN;
+  const long long total = npix * (C / 4);
+  hipLaunchKernelGGL(add_relu_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, a, a_cs, a_co, b, b_cs, b_co,
+                     out, o_cs, o_co, C / 4, relu, total);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_nchw_to_nhwc_f32(const float* in, int B, int C, int H, int W, float* out, int o_cs, int o_co,
+                                   void* stream) {
+  if (!in || !out) return KRRN_EARG;
+  if (B < 1 || C < 1 || H < 1 || W < 1 || o_co + C > o_cs) return KRRN_ESHAPE;
+  const long long total = (long long)B * C * H * W;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, in, C, H * W, out, o_cs,
+                     o_co, total);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_heads_select_f32(const float* fx, int Cx, int xyz_off, const float* fn, int Cn,
+                                   const long long* cls, float* xyz_out, float* nml_out, int B, int H, int W,
+                                   void* stream) {
+  if (!fx || !fn || !cls || !xyz_out || !nml_out) return KRRN_EARG;
+  if (B < 1 || H < 1 || W < 1 || Cx < xyz_off + 3 || Cn < 3) return KRRN_ESHAPE;
+  const long long total = (long long)B * H * W;
+  hipLaunchKernelGGL(heads_select_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, fx, Cx, xyz_off, fn, Cn,
+                     cls, xyz_out, nml_out, H * W, total);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_points_gather_f32(const float* cloud, const float* xyz, const float* nml, const long long* choose,
+                                    int B, int N, int H, int W, float* p9, void* stream) {
+  if (!cloud || !xyz || !nml || !choose || !p9) return KRRN_EARG;
+  if (B < 1 || N < 1 || H < 1 || W < 1) return KRRN_ESHAPE;
+  const long long total = (long long)B * N;
+  hipLaunchKernelGGL(points_gather_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, cloud, xyz, nml, choose,
+                     N, H * W, p9, total);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_gather_rows_f32(const void* idx, int idx64, long long idx_bs, int nrows, const float* src,
+                                  long long src_bs, int src_st, float* dst, long long dst_bs, int dst_st, int width,
+                                  int B, void* stream) {
+  if (!idx || !src || !dst) return KRRN_EARG;
+  if (B < 1 || nrows < 1 || width < 1) return KRRN_ESHAPE;
+  const bool vec = !(width & 3) && !(src_st & 3) && !(dst_st & 3) && !(src_bs & 3) && !(dst_bs & 3) &&
+                   krrn_aligned16(src) && krrn_aligned16(dst);
+  const long long total = (long long)B * nrows * (vec ? width / 4 : width);
+  hipStream_t s = (hipStream_t)stream;
+#define KRRN_GR(I64, V)                                                                                    \
+  hipLaunchKernelGGL((gather_rows_kernel<I64, V>), grid1(total), dim3(256), 0, s, idx, idx_bs, nrows, src, \
+                     src_bs, src_st, dst, dst_bs, dst_st, width, total)
+  if (idx64) {
+    if (vec) KRRN_GR(true, true); else KRRN_GR(true, false);
+  } else {
+    if (vec) KRRN_GR(false, true); else KRRN_GR(false, false);
+  }
+#undef KRRN_GR
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const float* w4, const float* b4,
+                                 const float* cloud, float* pred_t, float* t_res, void* stream) {
+  if (!h || !w4 || !b4 || !cloud || !pred_t) return KRRN_EARG;
+  if (B < 1 || n < 1 || C < 1) return KRRN_ESHAPE;
+  hipLaunchKernelGGL(tbase_tail_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, h, n, C, w4, b4, cloud, pred_t,
+                     t_res);
+  return krrn_launch_status();
+}
