@@ -96,19 +96,23 @@ __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
         const float cn = p[D];
         const float d = mode == 0 ? ((inner * -2.f) + cn) + qn : (cn + qn) - 2.f * inner;
         if (d < thr) {
-          // branch-free insertion into the ascending list; strict '<' keeps the earlier
-          // (lower) index first among equal distances. Slots >= K are scratch.
-          float nd = d;
-          int ni = j0 + j;
+          // branch-free insertion into the ascending list: the new entry goes in front of the
+          // first strictly larger one (so equal distances keep the earlier = lower index
+          // first) and every later slot takes its predecessor. Slots >= K are scratch.
+          const int ni = j0 + j;
+          bool ins = false;
+          float cd = 0.f;
+          int ci = 0;
 #pragma unroll
           for (int s = 0; s < kKnnKmax; ++s) {
-            const bool sw = nd < bd[s];
-            const float td = bd[s];
-            const int ti = bi[s];
-            bd[s] = sw ? nd : td;
-            bi[s] = sw ? ni : ti;
-            nd = sw ? td : nd;
-            ni = sw ? ti : ni;
+            const bool here = !ins && (d < bd[s]);
+            const float od = bd[s];
+            const int oi = bi[s];
+            bd[s] = ins ? cd : (here ? d : od);
+            bi[s] = ins ? ci : (here ? ni : oi);
+            cd = od;
+            ci = oi;
+            ins = ins || here;
           }
           float tv = INFINITY;
 #pragma unroll

@@ -1,0 +1,366 @@
+"""HRNet backbone of KRRN (lib/network/hrnet/myhrnet.py:28-527), MI355X execution.
+
+The nn.Module tree below only *holds parameters*, with exactly the reference's attribute
+names and nn.Sequential positions so that reference checkpoints load unchanged
+(`backbone.conv1`, `backbone.layer1.0.downsample.1`, `backbone.stage3.2.fuse_layers.2.0.1.0`,
+`backbone.last_layer.0.0`, `backbone.deconv_layer.1.0.conv1`, ...). The forward
+is compiled by `build_hrnet_plan` into NHWC HIP launches:
+
+  * every conv + eval-BN (+ residual add) (+ ReLU) is ONE implicit-GEMM launch
+    (krrn_conv2d_f32) with BN folded into a per-channel scale/bias;
+  * the multi-resolution fuse (myhrnet.py:226-250) accumulates into the output branch
+    buffer: j < i chains end in a conv whose epilogue adds the running sum, j > i terms
+    are a 1x1 conv at the low resolution followed by one bilinear-resize-add launch
+    (align_corners=False, myhrnet.py:242-245), the last term applies the ReLU;
+  * the final upsample + concat (myhrnet.py:511-516) resizes each branch straight into
+    its channel slice of the concat buffer, and last_layer / deconv_layer (:518-525)
+    write into channel slices so no torch.cat ever copies.
+Channel counts that are not multiples of 4 (W18: 18, 36, ...) are padded to 4 in memory;
+pad channels are exactly zero and the packed weights map logical -> physical channels.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .config import load_hrnet_spec
+from .ops import Act, pad4
+from .runtime import Plan, ptr
+
+BN_MOMENTUM = 0.1
+
+
+def conv3x3(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, kernel_size=3, stride=stride, padding=1, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.bn1 = nn.BatchNorm2d(planes, momentum=BN_MOMENTUM)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = conv3x3(planes, planes)
+        self.bn2 = nn.BatchNorm2d(planes, momentum=BN_MOMENTUM)
+        self.downsample = downsample
+        self.stride = stride
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, kernel_size=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes, momentum=BN_MOMENTUM)
+        self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes, momentum=BN_MOMENTUM)
+        self.conv3 = nn.Conv2d(planes, planes * 4, kernel_size=1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4, momentum=BN_MOMENTUM)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+
+class HighResolutionModule(nn.Module):
+    def __init__(self, num_branches, blocks, num_inchannels, num_channels):
+        super().__init__()
+        if not (num_branches == len(blocks) == len(num_inchannels) == len(num_channels)):
+            raise ValueError("HRNet stage spec: branch count mismatch")
+        self.num_branches = num_branches
+        self.num_inchannels = list(num_inchannels)
+        branches = []
+        for i in range(num_branches):
+            down = None
+            if self.num_inchannels[i] != num_channels[i]:
+                down = nn.Sequential(nn.Conv2d(self.num_inchannels[i], num_channels[i], 1, 1, bias=False),
+                                     nn.BatchNorm2d(num_channels[i], momentum=BN_MOMENTUM))
+            layers = [BasicBlock(self.num_inchannels[i], num_channels[i], 1, down)]
+            self.num_inchannels[i] = num_channels[i]
+            for _ in range(1, blocks[i]):
+                layers.append(BasicBlock(self.num_inchannels[i], num_channels[i]))
+            branches.append(nn.Sequential(*layers))
+        self.branches = nn.ModuleList(branches)
+        self.fuse_layers = self._make_fuse_layers() if num_branches > 1 else None
+        self.relu = nn.ReLU(True)
+
+    def _make_fuse_layers(self):
+        nb, ch = self.num_branches, self.num_inchannels
+        fuse = []
+        for i in range(nb):
+            row = []
+            for j in range(nb):
+                if j > i:
+                    row.append(nn.Sequential(nn.Conv2d(ch[j], ch[i], 1, 1, 0, bias=False),
+                                             nn.BatchNorm2d(ch[i], momentum=BN_MOMENTUM)))
+                elif j == i:
+                    row.append(None)
+                else:
+                    chain = []
+                    for k in range(i - j):
+                        last = k == i - j - 1
+                        cout = ch[i] if last else ch[j]
+                        mods = [nn.Conv2d(ch[j], cout, 3, 2, 1, bias=False), nn.BatchNorm2d(cout, momentum=BN_MOMENTUM)]
+                        if not last:
+                            mods.append(nn.ReLU(True))
+                        chain.append(nn.Sequential(*mods))
+                    row.append(nn.Sequential(*chain))
+            fuse.append(nn.ModuleList(row))
+        return nn.ModuleList(fuse)
+
+
+class HRNet(nn.Module):
+    """Parameter container with the reference's module names (myhrnet.py:258-346)."""
+
+    def __init__(self, spec, backbone_outc: int):
+        super().__init__()
+        self.spec = spec
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=3, stride=2, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(64, momentum=BN_MOMENTUM)
+        self.conv2 = nn.Conv2d(64, 64, kernel_size=3, stride=2, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(64, momentum=BN_MOMENTUM)
+        self.relu = nn.ReLU(inplace=True)
+        down = nn.Sequential(nn.Conv2d(64, 256, 1, 1, bias=False), nn.BatchNorm2d(256, momentum=BN_MOMENTUM))
+        self.layer1 = nn.Sequential(Bottleneck(64, 64, 1, down), *[Bottleneck(256, 64) for _ in range(3)])
+        pre = [256]
+        self.stage_branches: List[int] = []
+        for si, st in enumerate(spec.stages):
+            widths = list(st.widths)
+            setattr(self, f"transition{si + 1}", self._make_transition(pre, widths))
+            mods = []
+            inch = list(widths)
+            for _ in range(st.modules):
+                m = HighResolutionModule(len(widths), list(st.blocks), inch, widths)
+                mods.append(m)
+                inch = m.num_inchannels
+            setattr(self, f"stage{si + 2}", nn.Sequential(*mods))
+            pre = inch
+            self.stage_branches.append(len(widths))
+        L = sum(pre)
+        self.last_inp_channels = L
+        self.last_layer = nn.ModuleList([
+            nn.Sequential(nn.Conv2d(L, L, kernel_size=(3, 3), stride=(1, 1), padding='same'),
+                          nn.BatchNorm2d(L, momentum=BN_MOMENTUM), nn.ReLU(True)),
+            nn.Conv2d(L, backbone_outc, kernel_size=(1, 1), stride=(1, 1), padding=0)])
+        self.deconv_layer = nn.ModuleList([
+            nn.Sequential(nn.ConvTranspose2d(L + backbone_outc, backbone_outc, kernel_size=(4, 4), stride=(2, 2),
+                                             padding=(1, 1), bias=False),
+                          nn.BatchNorm2d(backbone_outc, eps=1e-05, momentum=0.1), nn.ReLU(True)),
+            nn.Sequential(BasicBlock(backbone_outc, backbone_outc))])
+        self.backbone_outc = backbone_outc
+
+    @staticmethod
+    def _make_transition(pre: List[int], cur: List[int]):
+        layers = []
+        for i in range(len(cur)):
+            if i < len(pre):
+                if cur[i] != pre[i]:
+                    layers.append(nn.Sequential(nn.Conv2d(pre[i], cur[i], 3, 1, 1, bias=False),
+                                                nn.BatchNorm2d(cur[i]), nn.ReLU(True)))
+                else:
+                    layers.append(None)
+            else:
+                chain = []
+                for j in range(i + 1 - len(pre)):
+                    cin = pre[-1]
+                    cout = cur[i] if j == i - len(pre) else cin
+                    chain.append(nn.Sequential(nn.Conv2d(cin, cout, 3, 2, 1, bias=False), nn.BatchNorm2d(cout),
+                                               nn.ReLU(True)))
+                layers.append(nn.Sequential(*chain))
+        return nn.ModuleList(layers)
+
+
+def build_hrnet(cfg) -> HRNet:
+    """build_modeifed_hrnet(config, cfg_name) equivalent (myhrnet.py:538-547)."""
+    return HRNet(load_hrnet_spec(cfg.Module.BACKBONE), cfg.Module.BACKBONE_OUTC)
+
+
+# ---------------------------------------------------------------------------------------
+# Plan compilation
+# ---------------------------------------------------------------------------------------
+
+class _Builder:
+    def __init__(self, plan: Plan, B: int):
+        self.plan = plan
+        self.B = B
+        self.dev = plan.device
+        self.specs = []  # keep folded weights alive
+
+    def act(self, H, W, c, cs=None) -> Act:
+        cs = pad4(c) if cs is None else cs
+        t = self.plan.buf((self.B, H, W, cs))
+        return Act(t, self.B, H, W, cs, 0, c)
+
+    def conv(self, x: Act, conv: nn.Module, bn: Optional[nn.Module], out: Optional[Act] = None,
+             res: Optional[Act] = None, relu: bool = False, cin_map=None) -> Act:
+        if isinstance(conv, nn.ConvTranspose2d):
+            spec = ops.make_convT(conv, bn, self.dev, cin_map=cin_map, cin_p=x.cp)
+        else:
+            spec = ops.make_conv(conv, bn, self.dev, cin_map=cin_map, cin_p=x.cp)
+        self.specs.append(spec)
+        Ho, Wo = ops.conv_out_hw(spec, x.H, x.W)
+        if out is None:
+            out = self.act(Ho, Wo, spec.cout)
+        assert (out.H, out.W) == (Ho, Wo) and out.cp >= pad4(spec.cout)
+        self.emit_conv(x, spec, out, res, relu)
+        return out
+
+    def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool):
+        np_ = pad4(spec.cout)
+        for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off)):
+            if spec.kind == "conv":
+                Hg, Wg, in_s, osy, osx = out.H, out.W, spec.stride, 1, 1
+            else:
+                Hg, Wg, in_s, osy, osx = x.H, x.W, 1, 2, 2
+            self.plan.add("krrn_conv2d_f32",
+                          ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, Hg, Wg, in_s, len(taps),
+                          ops._int_array([t[0] for t in taps]), ops._int_array([t[1] for t in taps]),
+                          ptr(spec.wt[cls]), np_, np_, ptr(spec.scale), ptr(spec.bias), ptr(None), 1,
+                          ptr(res.t if res is not None else None), res.cs if res is not None else 0,
+                          res.co if res is not None else 0, ptr(out.t), out.cs, out.co, out.H, out.W,
+                          osy, osx, ooy, oox, int(relu), 0, 0)
+
+    def resize(self, x: Act, out: Act, add: Optional[Act] = None, align: bool = False, relu: bool = False):
+        assert x.cp == out.cp
+        self.plan.add("krrn_resize_bilinear_f32", ptr(x.t), x.B, x.H, x.W, x.cs, x.co, x.cp, ptr(out.t), out.H,
+                      out.W, out.cs, out.co, ptr(add.t if add is not None else None),
+                      add.cs if add is not None else 0, add.co if add is not None else 0, int(align), int(relu))
+
+    def add_relu(self, a: Act, b: Optional[Act], out: Act, relu: bool = True):
+        self.plan.add("krrn_add_relu_f32", ptr(a.t), a.cs, a.co, ptr(b.t if b is not None else None),
+                      b.cs if b is not None else 0, b.co if b is not None else 0, ptr(out.t), out.cs, out.co,
+                      a.B * a.H * a.W, a.cp, int(relu))
+
+    # -- blocks ------------------------------------------------------------------------
+    def basic(self, x: Act, blk: BasicBlock, out: Optional[Act] = None) -> Act:
+        h = self.conv(x, blk.conv1, blk.bn1, relu=True)
+        res = x if blk.downsample is None else self.conv(x, blk.downsample[0], blk.downsample[1])
+        return self.conv(h, blk.conv2, blk.bn2, out=out, res=res, relu=True)
+
+    def bottleneck(self, x: Act, blk: Bottleneck) -> Act:
+        h = self.conv(x, blk.conv1, blk.bn1, relu=True)
+        h = self.conv(h, blk.conv2, blk.bn2, relu=True)
+        res = x if blk.downsample is None else self.conv(x, blk.downsample[0], blk.downsample[1])
+        return self.conv(h, blk.conv3, blk.bn3, res=res, relu=True)
+
+    def hr_module(self, xs: List[Act], m: HighResolutionModule, outs: Optional[List[Optional[Act]]] = None) -> List[Act]:
+        ys = []
+        for i, x in enumerate(xs):
+            for blk in m.branches[i]:
+                x = self.basic(x, blk)
+            ys.append(x)
+        if m.num_branches == 1:
+            return ys
+        fused = []
+        nb = m.num_branches
+        for i in range(nb):
+            out = outs[i] if outs is not None and outs[i] is not None else self.act(ys[i].H, ys[i].W, ys[i].c)
+            terms = [j for j in range(nb)]
+            acc: Optional[Act] = None  # running sum lives in `out` once written
+            for idx_t, j in enumerate(terms):
+                last = idx_t == nb - 1
+                if j == i:
+                    if acc is None:
+                        acc = ys[i]  # identity term: read in place, no copy
+                    elif last:
+                        self.add_relu(acc, ys[i], out, relu=True)
+                        acc = out
+                    else:
+                        self.add_relu(acc, ys[i], out, relu=False)
+                        acc = out
+                elif j > i:
+                    seq = m.fuse_layers[i][j]
+                    low = self.conv(ys[j], seq[0], seq[1])
+                    if acc is None:
+                        self.resize(low, out, add=None, align=False, relu=last)
+                    else:
+                        self.resize(low, out, add=acc, align=False, relu=last)
+                    acc = out
+                else:
+                    chain = m.fuse_layers[i][j]
+                    h = ys[j]
+                    for k, sub in enumerate(chain):
+                        final = k == len(chain) - 1
+                        if final:
+                            h = self.conv(h, sub[0], sub[1], out=out, res=acc, relu=last)
+                        else:
+                            h = self.conv(h, sub[0], sub[1], relu=True)
+                    acc = out
+            fused.append(out)
+        return fused
+
+
+def build_hrnet_plan(net: HRNet, plan: Plan, x: Act) -> Tuple[Act, Act, list]:
+    """Emit the HRNet forward (myhrnet.py:471-527) for input act `x`; returns (x_out @S/4, y_out @S/2)."""
+    bld = _Builder(plan, x.B)
+    h = bld.conv(x, net.conv1, net.bn1, relu=True)
+    h = bld.conv(h, net.conv2, net.bn2, relu=True)
+    for blk in net.layer1:
+        h = bld.bottleneck(h, blk)
+    ylist = [h]
+    nstages = len(net.spec.stages)
+    for si in range(nstages):
+        trans = getattr(net, f"transition{si + 1}")
+        stage = getattr(net, f"stage{si + 2}")
+        nb = net.stage_branches[si]
+        xl = []
+        for i in range(nb):
+            t = trans[i]
+            if t is None:
+                xl.append(ylist[i])
+            else:
+                # myhrnet.py:482-507: transition1 reads the stem output; transition2 reads
+                # y_list[-1] for every non-None entry; transition3 reads y_list[i] for
+                # i < NUM_BRANCHES(stage3) and y_list[-1] otherwise.
+                if si == 0:
+                    src = ylist[0]
+                elif si == 1:
+                    src = ylist[-1]
+                else:
+                    src = ylist[i] if i < len(ylist) else ylist[-1]
+                chain = [t] if isinstance(t[0], nn.Conv2d) else list(t)
+                for sub in chain:
+                    src = bld.conv(src, sub[0], sub[1], relu=True)
+                xl.append(src)
+        for mi, m in enumerate(stage):
+            xl = bld.hr_module(xl, m)
+        ylist = xl
+    # upsample + concat (myhrnet.py:511-516) straight into channel slices
+    H0, W0 = ylist[0].H, ylist[0].W
+    widths = [y.c for y in ylist]
+    offs, o = [], 0
+    for w in widths:
+        offs.append(o)
+        o += pad4(w)
+    Lp = o
+    L = sum(widths)
+    # concat buffer: [cat(y0..y3) (Lp physical) | last_layer_1 out (L) | last_layer_2 out (C_b)]
+    Cb = net.backbone_outc
+    cat = bld.act(H0, W0, Lp, cs=Lp)
+    for k, y in enumerate(ylist):
+        dst = cat.slice(offs[k], y.c)
+        if k == 0:
+            bld.add_relu(y, None, dst, relu=False)
+        else:
+            bld.resize(y, dst, align=False)
+    cat_map = []
+    for k, w in enumerate(widths):
+        cat_map += list(range(offs[k], offs[k] + w))
+    # last_layer: conv3x3 'same' + bias + BN + ReLU (L -> L), then conv1x1 + bias (L -> C_b);
+    # y = cat(x_list) = [last_layer_1 out, last_layer_2 out] (myhrnet.py:518-522)
+    Lpp = pad4(L)
+    ycat = bld.act(H0, W0, Lpp + pad4(Cb), cs=Lpp + pad4(Cb))
+    x1 = ycat.slice(0, L)
+    bld.conv(cat, net.last_layer[0][0], net.last_layer[0][1], out=x1, relu=True, cin_map=cat_map)
+    x2 = ycat.slice(Lpp, Cb)
+    bld.conv(x1, net.last_layer[1], None, out=x2, relu=False)
+    ycat_map = list(range(L)) + list(range(Lpp, Lpp + Cb))
+    ycat_full = Act(ycat.t, ycat.B, ycat.H, ycat.W, ycat.cs, 0, Lpp + pad4(Cb))
+    d = bld.conv(ycat_full, net.deconv_layer[0][0], net.deconv_layer[0][1], relu=True, cin_map=ycat_map)
+    y = bld.basic(d, net.deconv_layer[1][0])
+    return x2, y, bld.specs

@@ -1,0 +1,232 @@
+"""KRRN dense-fusion model (lib/network/krrn.py:27-165) — the drop-in model API.
+
+    model = KRRN(num_cls=1, cfg=CONFIG).cuda().eval()
+    model.load_state_dict(state_dict)          # reference checkpoint keys
+    pred = model(x, p_emb, choose, cls, region_point=None, opt_pose=True)
+    pred -> {'xyz', 'region', 'mask', 'normal', 'pred_r' (None), 'pred_t'}
+
+The modules hold parameters only. On the first call for a given (B, S, N) a launch plan is
+compiled (runtime.Plan): HRNet (hrnet.py) -> heads -> class select / normalise -> choose
+gather -> FusionNetLite (fusion.py) -> TBase (posenet.py), ~400 HIP launches over plan-owned
+NHWC workspaces. Every arithmetic step runs in libkrrn_hip.so; torch only allocates memory,
+copies the caller's tensors into the plan's static input buffers and provides the stream.
+
+Randomness (the five torch.randperm draws of the Pool_layers, gcn3d.py:239):
+  perm_mode='host'   (default) torch.randperm on the CPU generator in the reference's order
+                     (pool_1_v, pool_1_x, pool_1_n, pool_1, pool_2), one per forward,
+                     shared by the batch — reference semantics;
+  perm_mode='device' counter-based draws on the GPU (krrn_randperm_i32), for graph replay;
+  perms=[...]        explicit permutations (parity tests).
+Outputs are views of plan-owned buffers that the next forward of the same shape overwrites
+(CUDA-graph static-output semantics); clone them to keep them.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .config import CONFIG
+from .fusion import FusionNetLite, build_fusion_plan, level_sizes
+from .hrnet import _Builder, build_hrnet, build_hrnet_plan
+from .ops import Act, pad4
+from .posenet import PoseNet, build_tbase_plan
+from .runtime import Late, Plan, ptr
+
+
+class KRRNPlan:
+    """Compiled forward for one (B, S, N, opt_pose)."""
+
+    def __init__(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device):
+        self.B, self.S, self.N, self.opt_pose = B, S, N, opt_pose
+        cfg = model.cfg
+        C = model.num_cls
+        plan = Plan(device)
+        self.plan = plan
+        # static inputs
+        self.x_in = plan.buf((B, 3, S, S))
+        self.cloud = plan.buf((B, N, 3))
+        self.choose = plan.buf((B, 1, N), torch.int64)
+        self.cls = plan.buf((B, 1), torch.int64)
+        self.seed = torch.zeros(1, dtype=torch.int64, device=device)
+        xa = Act(plan.buf((B, S, S, 4)), B, S, S, 4, 0, 3)
+        plan.add("krrn_nchw_to_nhwc_f32", ptr(self.x_in), B, 3, S, S, ptr(xa.t), 4, 0)
+        xmap, ymap, specs = build_hrnet_plan(model.backbone, plan, xa)
+        bld = _Builder(plan, B)
+        # XYZNet (krrn.py:46-65): ConvT s2 + BN + ReLU, conv + BN + ReLU, x2 bilinear
+        # (align_corners=True), 2 x (conv + BN + ReLU), then xyz_final (1x1 + bias)
+        X = model.XYZNet
+        h = bld.conv(xmap, X[0], X[1], relu=True)
+        h = bld.conv(h, X[3], X[4], relu=True)
+        up = bld.act(2 * h.H, 2 * h.W, h.c)
+        bld.resize(h, up, align=True)
+        h = bld.conv(up, X[7], X[8], relu=True)
+        h = bld.conv(h, X[10], X[11], relu=True)
+        self.xyz_outc = model.xyz_outc
+        self.fx = plan.buf((B, model.xyz_outc, h.H, h.W))
+        spec = ops.make_conv(model.xyz_final, None, device, cin_p=h.cp)
+        bld.specs.append(spec)
+        self._nchw_conv(h, spec, self.fx, model.xyz_outc)
+        # NMLNet (krrn.py:68-84)
+        Nn = model.NMLNet
+        g = bld.conv(ymap, Nn[0], Nn[1], relu=True)
+        g = bld.conv(g, Nn[3], Nn[4], relu=True)
+        upn = bld.act(2 * g.H, 2 * g.W, g.c)
+        bld.resize(g, upn, align=True)
+        g = bld.conv(upn, Nn[7], Nn[8], relu=True)
+        self.fn = plan.buf((B, 3 * C, g.H, g.W))
+        spec_n = ops.make_conv(model.nml_final, None, device, cin_p=g.cp)
+        bld.specs.append(spec_n)
+        self._nchw_conv(g, spec_n, self.fn, 3 * C)
+        Ho, Wo = h.H, h.W
+        self.Ho, self.Wo = Ho, Wo
+        # class gather + F.normalize (krrn.py:100-108)
+        self.xyz = plan.buf((B, 3, Ho, Wo))
+        self.normal = plan.buf((B, 3, Ho, Wo))
+        plan.add("krrn_heads_select_f32", ptr(self.fx), model.xyz_outc, model.region_outc, ptr(self.fn), 3 * C,
+                 ptr(self.cls), ptr(self.xyz), ptr(self.normal), B, Ho, Wo)
+        self.specs = [specs, bld.specs]
+        self.pred_t = None
+        if opt_pose:
+            # choose gather (krrn.py:121-122) -> P9 = [cloud | xyz_emb | nml_emb]
+            self.p9 = plan.buf((B, N, 9))
+            plan.add("krrn_points_gather_f32", ptr(self.cloud), ptr(self.xyz), ptr(self.normal), ptr(self.choose), B, N,
+                     Ho, Wo, ptr(self.p9))
+            N1, N2, _, _ = level_sizes(N, model.fusion.neighbor_num)
+            self.perm_sizes = [("v", N, N1), ("x", N, N1), ("n", N, N1), ("p1", N, N1), ("p2", N1, N2)]
+            self.perms = {k: plan.buf((m,), torch.int32) for k, _, m in self.perm_sizes}
+            self.perm_ops_start = len(plan)
+            self.device_perm_plan = Plan(device)
+            for sid, (k, n, m) in enumerate(self.perm_sizes):
+                self.device_perm_plan.add("krrn_randperm_i32", ptr(self.seed), sid, n, m, 1, ptr(self.perms[k]))
+            feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms)
+            self.feat = feat
+            self.pred_t, self.tbase_bufs = build_tbase_plan(model.pose.t_net, plan, B, N, feat, "cls", "cloud",
+                                                            cfg.Module.POSENet.INC_R, C)
+        self.env = {"cls": self.cls, "cloud": self.cloud}
+
+    def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):
+        taps = spec.taps[0]
+        B, Cx, Ho, Wo = out.shape
+        self.plan.add("krrn_conv2d_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, Ho, Wo, spec.stride,
+                      len(taps), ops._int_array([t[0] for t in taps]), ops._int_array([t[1] for t in taps]),
+                      ptr(spec.wt[0]), pad4(spec.cout), n_store, ptr(spec.scale), ptr(spec.bias), ptr(None), 1,
+                      ptr(None), 0, 0, ptr(out), Cx, 0, Ho, Wo, 1, 1, 0, 0, 0, 1, 0)
+
+    # ------------------------------------------------------------------------------------
+    def load_inputs(self, x, p_emb, choose, cls):
+        self.x_in.copy_(x, non_blocking=True)
+        if self.opt_pose:
+            self.cloud.copy_(p_emb, non_blocking=True)
+            self.choose.copy_(choose.reshape(self.B, 1, self.N), non_blocking=True)
+        self.cls.copy_(cls.reshape(self.B, 1), non_blocking=True)
+
+    def set_perms(self, perms: Optional[Sequence[torch.Tensor]], mode: str):
+        if not self.opt_pose:
+            return
+        if perms is not None:
+            for (k, n, m), p in zip(self.perm_sizes, perms):
+                self.perms[k].copy_(p.reshape(-1)[:m].to(torch.int32), non_blocking=True)
+        elif mode == "host":
+            # torch.randperm(vertice_num)[:pool_num] on the CPU generator, in module call order
+            for k, n, m in self.perm_sizes:
+                self.perms[k].copy_(torch.randperm(n)[:m].to(torch.int32), non_blocking=True)
+        elif mode == "device":
+            self.device_perm_plan.run({})
+        else:
+            raise ValueError(f"perm_mode {mode!r}")
+
+    def run(self):
+        self.plan.run(self.env)
+
+    def outputs(self, model: "KRRN") -> Dict[str, Optional[torch.Tensor]]:
+        C = model.num_cls
+        return {
+            "xyz": self.xyz,
+            "region": self.fx[:, model.mask_outc:model.region_outc],
+            "mask": self.fx[:, 0:model.mask_outc],
+            "normal": self.normal,
+            "pred_r": None,
+            "pred_t": self.pred_t if self.opt_pose else None,
+        }
+
+
+class KRRN(nn.Module):
+    def __init__(self, num_cls: int = 1, cfg=CONFIG):
+        super().__init__()
+        self.cfg = cfg
+        self.num_cls = cfg.Module.NUM_CLS  # the reference ignores num_cls too (krrn.py:30)
+        self.backbone = build_hrnet(cfg)
+        xyz_channels = cfg.Module.XYZNet.HEADEN_FS
+        mask_out = cfg.Module.MASKNet.OUT_FS * self.num_cls + 1
+        xyz_out = cfg.Module.XYZNet.OUT_FS * self.num_cls
+        region_out = cfg.Module.REGIONNet.OUT_FS
+        self.mask_outc = mask_out
+        self.region_outc = mask_out + region_out
+        self.xyz_outc = mask_out + xyz_out + region_out
+        nml_channels = cfg.Module.NMLNet.HEADEN_FS
+        nml_out = cfg.Module.NMLNet.OUT_FS * self.num_cls
+        Cb = cfg.Module.BACKBONE_OUTC
+        bn = lambda c: nn.BatchNorm2d(c, eps=1e-05, momentum=0.1, affine=True, track_running_stats=True)  # noqa: E731
+        self.XYZNet = nn.Sequential(
+            nn.ConvTranspose2d(Cb, xyz_channels, kernel_size=(3, 3), stride=(2, 2), padding=(1, 1),
+                               output_padding=(1, 1), bias=False),
+            bn(xyz_channels), nn.ReLU(inplace=True),
+            nn.Conv2d(xyz_channels, xyz_channels, (3, 3), (1, 1), (1, 1), bias=False), bn(xyz_channels),
+            nn.ReLU(inplace=True),
+            nn.UpsamplingBilinear2d(scale_factor=2.0),
+            nn.Conv2d(xyz_channels, xyz_channels, (3, 3), (1, 1), (1, 1), bias=False), bn(xyz_channels),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(xyz_channels, xyz_channels, (3, 3), (1, 1), (1, 1), bias=False), bn(xyz_channels),
+            nn.ReLU(inplace=True))
+        self.xyz_final = nn.Conv2d(xyz_channels, self.xyz_outc, kernel_size=(1, 1))
+        self.NMLNet = nn.Sequential(
+            nn.Conv2d(Cb, nml_channels, (3, 3), (1, 1), (1, 1), bias=False), bn(nml_channels), nn.ReLU(inplace=True),
+            nn.Conv2d(nml_channels, nml_channels, (3, 3), (1, 1), (1, 1), bias=False), bn(nml_channels),
+            nn.ReLU(inplace=True),
+            nn.UpsamplingBilinear2d(scale_factor=2.0),
+            nn.Conv2d(nml_channels, nml_channels, (3, 3), (1, 1), (1, 1), bias=False), bn(nml_channels),
+            nn.ReLU(inplace=True))
+        self.nml_final = nn.Conv2d(nml_channels, nml_out, kernel_size=(1, 1))
+        self.fusion = FusionNetLite(cfg)
+        self.pose = PoseNet(cfg)
+        self._plans: Dict[Tuple, KRRNPlan] = {}
+        self.perm_mode = "host"
+
+    # plans fold the weights: any weight change invalidates them
+    def invalidate_plans(self):
+        self._plans.clear()
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        self.invalidate_plans()
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def _apply(self, fn, *args, **kwargs):
+        self.invalidate_plans()
+        return super()._apply(fn, *args, **kwargs)
+
+    def get_plan(self, B: int, S: int, N: int, opt_pose: bool = True) -> KRRNPlan:
+        key = (B, S, N, bool(opt_pose))
+        p = self._plans.get(key)
+        if p is None:
+            dev = next(self.parameters()).device
+            if dev.type != "cuda":
+                raise RuntimeError("KRRN runs on the MI355X HIP path only: call .cuda() first")
+            with torch.no_grad():
+                p = KRRNPlan(self, B, S, N, opt_pose, dev)
+            self._plans[key] = p
+        return p
+
+    @torch.no_grad()
+    def forward(self, x, p_emb, choose, cls, region_point=None, opt_pose=True, perms=None):
+        B, _, S, S2 = x.shape
+        if S != S2:
+            raise ValueError("KRRN crops are square (batchdataset.py:890-961)")
+        N = p_emb.shape[1] if opt_pose else 1
+        p = self.get_plan(B, S, N, opt_pose)
+        p.load_inputs(x, p_emb, choose, cls)
+        p.set_perms(perms, self.perm_mode)
+        p.run()
+        return p.outputs(self)

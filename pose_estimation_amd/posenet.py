@@ -1,0 +1,76 @@
+"""Translation head of KRRN (lib/network/pose/posenet.py:51-96), MI355X execution.
+
+TBase = Conv1d(1280 + C -> 1024) + BN + ReLU -> (-> 256) + BN + ReLU -> (-> 256) + BN + ReLU
+        -> Dropout (eval: identity) -> Conv1d(-> OUT_T); t_res = [:, 0:3]
+and KRRN.forward's pred_t = mean_N(p_emb + t_res) (krrn.py:153).
+
+Execution: the one-hot class channels of the concat (krrn.py:132-138) contribute exactly the
+column W1[:, 1280 + cls] to conv1, so they become a per-crop bias (one gather launch) instead
+of C extra input channels; conv1..conv3 are f32-MFMA GEMMs with BN folded into the epilogue;
+conv4 + the mean over points is one reduction launch per crop.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .runtime import Late, Plan, ptr
+
+
+class TBase(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.f = cfg.Module.POSENet.INC_R + cfg.Module.NUM_CLS
+        self.k = cfg.Module.POSENet.OUT_T
+        self.conv1 = nn.Conv1d(self.f, 1024, 1)
+        self.conv2 = nn.Conv1d(1024, 256, 1)
+        self.conv3 = nn.Conv1d(256, 256, 1)
+        self.conv4 = nn.Conv1d(256, self.k, 1)
+        self.drop1 = nn.Dropout(0.2)
+        self.bn1 = nn.BatchNorm1d(1024)
+        self.bn2 = nn.BatchNorm1d(256)
+        self.bn3 = nn.BatchNorm1d(256)
+
+
+class PoseNet(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.t_net = TBase(cfg)
+
+
+def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, cls_key: str, cloud_key: str,
+                     inc_r: int, num_cls: int):
+    """Emit TBase + pred_t. `feat` is [B, N, inc_r]; cls ([B, 1] int64) and cloud ([B, N, 3])
+    are late-bound env tensors. Returns the [B, 3] pred_t buffer."""
+    dev = plan.device
+    w1 = tb.conv1.weight.detach()[:, :, 0]
+    spec1 = ops.make_linear(w1[:, :inc_r], tb.conv1.bias, tb.bn1, dev)
+    # one-hot columns, pre-multiplied by the folded BN scale: colv[c] = scale * W1[:, inc_r + c]
+    np1 = ops.pad4(1024)
+    colv = torch.zeros(num_cls, np1, device=dev)
+    colv[:, :1024] = (spec1.scale[:1024, None] * w1[:, inc_r:inc_r + num_cls].to(dev).float()).t()
+    spec2 = ops.make_linear(tb.conv2.weight, tb.conv2.bias, tb.bn2, dev)
+    spec3 = ops.make_linear(tb.conv3.weight, tb.conv3.bias, tb.bn3, dev)
+    w4 = tb.conv4.weight.detach()[:3, :, 0].float().contiguous().to(dev)
+    b4 = tb.conv4.bias.detach()[:3].float().contiguous().to(dev)
+    b2 = plan.buf((B, np1))
+    h1 = plan.buf((B * N, 1024))
+    h2 = plan.buf((B * N, 256))
+    h3 = plan.buf((B * N, 256))
+    pred_t = plan.buf((B, 3))
+    M = B * N
+    plan.add("krrn_gather_rows_f32", Late(cls_key), 1, 1, 1, ptr(colv), 0, np1, ptr(b2), np1, np1, np1, B)
+
+    def gemm(a, K, spec, out, bias2=None):
+        np_ = ops.pad4(spec.cout)
+        plan.add("krrn_conv2d_f32", ptr(a), K, 0, 1, 1, M, spec.cin_p, 1, M, 1, 1, ops._int_array([0]),
+                 ops._int_array([0]), ptr(spec.wt[0]), np_, np_, ptr(spec.scale), ptr(spec.bias), ptr(bias2), N,
+                 ptr(None), 0, 0, ptr(out), out.shape[-1], 0, 1, M, 1, 1, 0, 0, 1, 0, 0)
+
+    gemm(feat, inc_r, spec1, h1, bias2=b2)
+    gemm(h1, 1024, spec2, h2)
+    gemm(h2, 256, spec3, h3)
+    plan.add("krrn_tbase_tail_f32", ptr(h3), B, N, 256, ptr(w4), ptr(b4), Late(cloud_key), ptr(pred_t), ptr(None))
+    plan.buffers.append([spec1, spec2, spec3, colv, w4, b4])
+    return pred_t, dict(h1=h1, h2=h2, h3=h3)

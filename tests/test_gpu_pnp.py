@@ -1,0 +1,110 @@
+"""Batched PnP-RANSAC kernel vs the C oracle (identical subsets) and known-answer recovery."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import pnp as opnp
+from pose_estimation_amd import pose
+
+pytestmark = pytest.mark.gpu
+
+K4 = np.array([572.4114, 573.57043, 325.2611, 242.04899], np.float32)
+
+
+def _scene(B, N, S, seed, outlier_frac=0.1, noise_px=0.0):
+    """xyz maps whose chosen pixels hold exact normalised model coordinates of a known pose."""
+    rng = np.random.default_rng(seed)
+    ext = np.array([0.067, 0.1276, 0.1175])
+    lfb = np.array([-0.0335, -0.0638, -0.0587])
+    xyz = np.zeros((B, 3, S, S), np.float32)
+    choose = np.zeros((B, 1, N), np.int64)
+    xm = np.zeros((B, N, 1), np.float32)
+    ym = np.zeros((B, N, 1), np.float32)
+    Rs, ts = [], []
+    for b in range(B):
+        R = opnp.rotation_from_axis_angle(rng.normal(size=3))
+        t = np.array([rng.uniform(-0.1, 0.1), rng.uniform(-0.1, 0.1), rng.uniform(0.7, 1.1)])
+        pix = rng.choice(S * S, N, replace=False)
+        u = rng.random((N, 3))
+        pw = (u * ext + lfb)
+        # store the f32 normalised coordinate the network would predict
+        u32 = u.astype(np.float32)
+        pw = u32.astype(np.float64) * ext + lfb
+        pc = pw @ R.T + t
+        img = np.stack([K4[0] * pc[:, 0] / pc[:, 2] + K4[2], K4[1] * pc[:, 1] / pc[:, 2] + K4[3]], 1)
+        img += rng.normal(scale=noise_px, size=img.shape) if noise_px else 0
+        out = rng.random(N) < outlier_frac
+        img[out] += rng.uniform(-20, 20, size=(out.sum(), 2))
+        flat = xyz[b].reshape(3, -1)
+        flat[:, pix] = u32.T
+        choose[b, 0] = pix
+        xm[b, :, 0] = img[:, 0]
+        ym[b, :, 0] = img[:, 1]
+        Rs.append(R)
+        ts.append(t)
+    data = {"choose": torch.from_numpy(choose), "x_map_choosed": torch.from_numpy(xm),
+            "y_map_choosed": torch.from_numpy(ym), "intrinsic": torch.from_numpy(np.tile(K4, (B, 1))),
+            "extent": torch.from_numpy(np.tile(ext, (B, 1))), "lfborder": torch.from_numpy(np.tile(lfb, (B, 1)))}
+    return torch.from_numpy(xyz), data, np.stack(Rs), np.stack(ts)
+
+
+def test_known_pose_recovery(dev):
+    B, N, S = 8, 1000, 120
+    xyz, data, Rgt, tgt = _scene(B, N, S, 0)
+    R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
+    torch.cuda.synchronize()
+    R, t = R.cpu().numpy(), t.cpu().numpy()
+    assert np.abs(R - Rgt).max() < 1e-3, np.abs(R - Rgt).max()
+    assert np.abs(t - tgt).max() < 1e-3
+    assert (info["inliers"].cpu().numpy() >= 200).all()
+
+
+def test_matches_oracle_same_subsets(dev):
+    B, N, S = 16, 1000, 100
+    xyz, data, _, _ = _scene(B, N, S, 1, outlier_frac=0.3, noise_px=0.4)
+    R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
+    torch.cuda.synchronize()
+    sel = info["sel"].cpu().long()
+    subs = info["subsets"].cpu()
+    for b in range(B):
+        s = sel[b]
+        pix = data["choose"][b, 0, s]
+        obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
+        img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
+        Ro, to, cnt, mask, bh = opnp.pnp_ransac(obj, img, K4, subs[b].numpy(), 1.0)
+        assert abs(int(info["inliers"][b]) - cnt) <= 2, (b, int(info["inliers"][b]), cnt)
+        assert np.abs(R[b].cpu().numpy() - Ro).max() < 1e-4
+        assert np.abs(t[b].cpu().numpy() - to).max() < 1e-4
+
+
+def test_ransac_failure_identity(dev):
+    # pure noise correspondences: no hypothesis reaches 5 inliers -> R = I, t = 0 (cv2 failure)
+    B, N, S = 2, 300, 40
+    xyz, data, _, _ = _scene(B, N, S, 2, outlier_frac=1.0)
+    data["x_map_choosed"] = torch.rand(B, N, 1) * 640
+    data["y_map_choosed"] = torch.rand(B, N, 1) * 480
+    R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
+    torch.cuda.synchronize()
+    for b in range(B):
+        if int(info["inliers"][b]) == 0:
+            assert torch.allclose(R[b].cpu(), torch.eye(3))
+            assert torch.all(t[b].cpu() == 0)
+
+
+def test_device_rng(dev):
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import ptr, P
+    seed = torch.tensor([123], dtype=torch.int64, device=dev)
+    out = torch.empty((4, 250), dtype=torch.int32, device=dev)
+    st = P(torch.cuda.current_stream().cuda_stream)
+    _lib.check(_lib.lib().krrn_randperm_i32(ptr(seed), 0, 1000, 250, 4, ptr(out), st), "randperm")
+    subs = torch.empty((3, 100, 5), dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().krrn_ransac_subsets(ptr(seed), 1, 3, 100, 256, ptr(subs), st), "subsets")
+    torch.cuda.synchronize()
+    o = out.cpu()
+    for r in range(4):
+        assert len(set(o[r].tolist())) == 250 and o[r].min() >= 0 and o[r].max() < 1000
+    assert not torch.equal(o[0], o[1])
+    s = subs.cpu().reshape(-1, 5)
+    assert all(len(set(row.tolist())) == 5 for row in s)
+    assert s.min() >= 0 and s.max() < 256
