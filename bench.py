@@ -1,0 +1,253 @@
+"""KRRN inference benchmark on MI355X (BASELINE.json metric: crops/s).
+
+A step = one pass of the hot path over one batch of synthetic LineMOD crops resident in HBM:
+HRNet-W18 + heads + class select/normalise + choose gather + FusionNetLite + TBase (pred_t)
++ batched PnP-RANSAC (R), including the device-side randomness (pool permutations, the 256-
+point PnP subset, RANSAC hypotheses). The whole step is one hipGraph replay. With --gpus N
+(torchrun, one process per GPU, RCCL) every rank runs its own batch (weak scaling) and the
+per-crop pose records are all-gathered over RCCL after every step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--size 120] [--points 1000]
+
+Rank 0 prints ONE JSON line (metric, value = crops/s over all ranks, roofline of the dominant
+kernel measured with HIP events, cpu_baseline = the CPU oracle on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from pose_estimation_amd.config import make_config  # noqa: E402
+from pose_estimation_amd.krrn import KRRN  # noqa: E402
+from pose_estimation_amd.pose import add_pose_ops  # noqa: E402
+from pose_estimation_amd.runtime import Plan, ptr  # noqa: E402
+from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
+
+METRIC = "crops/sec at 640×480 RGB-D, 1000 sampled pts; ADD(-S) AUC vs reference"
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+class Step:
+    """The full per-batch hot path over plan-owned static buffers."""
+
+    def __init__(self, model: KRRN, data, B: int, S: int, N: int, dev):
+        self.kp = model.get_plan(B, S, N, True)
+        kp = self.kp
+        kp.load_inputs(data["img_croped"].to(dev), data["cloud"].to(dev), data["choose"].to(dev),
+                       data["cls_id"].to(dev))
+        self.xm = data["x_map_choosed"].reshape(B, N).contiguous().to(dev)
+        self.ym = data["y_map_choosed"].reshape(B, N).contiguous().to(dev)
+        self.K4 = data["intrinsic"].contiguous().to(dev)
+        self.ext = data["extent"].double().contiguous().to(dev)
+        self.lfb = data["lfborder"].double().contiguous().to(dev)
+        self.pose_plan = Plan(dev)
+        self.R, self.t, self.inl, _ = add_pose_ops(self.pose_plan, kp.xyz, kp.choose.view(B, N), B, N, self.xm,
+                                                   self.ym, self.K4, self.ext, self.lfb, kp.seed)
+        self.pose_plan.add("krrn_rng_advance", ptr(kp.seed))
+        # per-crop pose record for the all-gather: R(9) t(3) pred_t(3) inliers(1) -> 16 f32 = 64 B
+        self.record = torch.zeros((B, 16), dtype=torch.float32, device=dev)
+        self.plans = [kp.device_perm_plan, kp.plan, self.pose_plan]
+
+    def run(self):
+        self.kp.device_perm_plan.run({})
+        self.kp.run()
+        self.pose_plan.run({})
+
+    def pack_record(self):
+        B = self.record.shape[0]
+        self.record[:, 0:9].copy_(self.R.view(B, 9))
+        self.record[:, 9:12].copy_(self.t)
+        self.record[:, 12:15].copy_(self.kp.pred_t)
+        self.record[:, 15].copy_(self.inl)
+
+    def profile(self):
+        """Per-op device time (HIP events around every launch, eager) -> list of (op, ms)."""
+        out = []
+        for p in (self.kp.device_perm_plan, self.kp.plan, self.pose_plan):
+            env = dict(self.kp.env) if p is self.kp.plan else {}
+            ms = p.run_timed(env)
+            out.extend(zip(p.ops, ms))
+        return out
+
+
+def roofline_from_profile(prof, B: int):
+    groups = {}
+    for op, ms in prof:
+        k = op.meta.get("kernel", op.name)
+        g = groups.setdefault(k, {"ms": 0.0, "flops": 0.0, "n": 0})
+        g["ms"] += ms
+        g["flops"] += op.meta.get("flops", 0.0)
+        g["n"] += 1
+    total_ms = sum(g["ms"] for g in groups.values())
+    dom = max(groups, key=lambda k: groups[k]["ms"])
+    g = groups[dom]
+    avg_ms = g["ms"] / g["n"]
+    achieved = (g["flops"] / g["n"]) / (avg_ms * 1e-3) / 1e12 if g["flops"] > 0 else None
+    conv_ms = sum(v["ms"] for k, v in groups.items() if k.startswith("conv_gemm"))
+    conv_fl = sum(v["flops"] for k, v in groups.items() if k.startswith("conv_gemm"))
+    breakdown = {k: {"ms": round(v["ms"], 4), "launches": v["n"],
+                     **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {})}
+                 for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])}
+    roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
+            "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4) if achieved else None, "traffic": None,
+            "launches": g["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
+            "flops_per_launch": round(g["flops"] / g["n"]),
+            "all_conv_gemm": {"ms_per_step": round(conv_ms, 3),
+                              "TFLOP/s": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2) if conv_ms else None,
+                              "GFLOP_per_crop": round(conv_fl / B / 1e9, 3)},
+            "events_ms_per_step": round(total_ms, 3)}
+    return roof, breakdown
+
+
+def cpu_baseline(B: int, S: int, N: int, backbone: str, budget_s: float):
+    """The CPU oracle (PyTorch-CPU restatement + C EPnP-RANSAC) on a bounded sample."""
+    from oracle.krrn_oracle import KRRNOracle, get_pose
+    from pose_estimation_amd.fusion import level_sizes
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    m = KRRN(cfg=make_config(num_cls=1, backbone=backbone))
+    sd = init_weights(m, 0)
+    o = KRRNOracle(num_cls=1, backbone=backbone)
+    o.load_state_dict(sd)
+    o.eval()
+    bcpu = 2
+    d = make_batch(bcpu, S, N, seed=99)
+    N1, N2, _, _ = level_sizes(N, 10)
+
+    def one():
+        perms = [torch.randperm(N)[:N1] for _ in range(4)] + [torch.randperm(N1)[:N2]]
+        pred = o(d["img_croped"], d["cloud"], d["choose"], d["cls_id"], perms=perms)
+        sel = torch.stack([torch.randperm(N)[:256] for _ in range(bcpu)])
+        subs = torch.stack([torch.stack([torch.randperm(256)[:5] for _ in range(100)]) for _ in range(bcpu)])
+        get_pose(pred, d, sel, subs.int())
+    one()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        n += bcpu
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": round(n / el, 4), "unit": "crops/s", "cores": threads, "kind": "port",
+            "sample": f"{n} crops ({n // bcpu} batches of {bcpu}), S={S}, N={N}, HRNet-{backbone}, oracle/krrn_oracle.py "
+                      f"f32 + oracle/pnp_ref.c EPnP-RANSAC H=100, {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--size", type=int, default=120)
+    ap.add_argument("--points", type=int, default=1000)
+    ap.add_argument("--backbone", default="w18")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--cpu-baseline-s", type=float, default=15.0)
+    ap.add_argument("--breakdown", default="", help="write the per-kernel breakdown JSON here")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B, S, N = args.batch, args.size, args.points
+
+    cfg = make_config(num_cls=1, backbone=args.backbone)
+    model = KRRN(cfg=cfg)
+    init_weights(model, 0)
+    model = model.to(dev).eval()
+    model.perm_mode = "device"
+    data = make_batch(B, S, N, seed=1 + rank)
+    step = Step(model, data, B, S, N, dev)
+    step.kp.seed.fill_(1000003 * (rank + 1))
+    gather_buf = torch.zeros((world * B, 16), dtype=torch.float32, device=dev) if world > 1 else None
+
+    step.run()  # eager warm-up (compiles nothing; touches every buffer)
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            step.run()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step.run()
+        torch.cuda.synchronize()
+
+    def one_step():
+        if graph is not None:
+            graph.replay()
+        else:
+            step.run()
+        if world > 1:
+            step.pack_record()
+            dist.all_gather_into_tensor(gather_buf, step.record)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms = el / args.steps * 1e3
+    value = world * B * args.steps / el
+
+    roof, breakdown = None, None
+    if rank == 0 and not args.no_profile:
+        step.profile()  # warm the eager path once
+        roof, breakdown = roofline_from_profile(step.profile(), B)
+        if args.breakdown:
+            with open(args.breakdown, "w") as f:
+                json.dump({"roofline": roof, "kernels": breakdown}, f, indent=1)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline_s > 0:
+        cpu = cpu_baseline(2, S, N, args.backbone, args.cpu_baseline_s)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded LineMOD-shaped crops, random-init weights)",
+            "config": {"workload": f"LineMOD 'cat' batch={B}/GPU, {S}x{S} crops from 640x480 RGB-D, "
+                                   f"HRNet-{args.backbone.upper()} + {N}-pt fusion + TBase, PnP-RANSAC (H=100) on GPU",
+                       "batch_per_gpu": B, "crop": S, "points": N, "backbone": f"hrnet_{args.backbone}",
+                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": graph is not None},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .runtime import Late, Plan, ptr
+from .runtime import Late, Plan, add_conv, ptr
 
 
 class Conv_surface(nn.Module):  # noqa: N801 (reference class name, gcn3d.py:72)
@@ -158,9 +158,10 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
                                cin_p=ops.pad4(layer.in_channel))
         keep.append(spec)
         np_ = ops.pad4(spec.cout)
-        plan.add("krrn_conv2d_f32", ptr(a), a_cs, a_co, 1, 1, M, spec.cin_p, 1, M, 1, 1, ops._int_array([0]),
-                 ops._int_array([0]), ptr(spec.wt[0]), np_, np_, ptr(spec.scale), ptr(spec.bias), ptr(None), 1,
-                 ptr(None), 0, 0, ptr(out), out.shape[-1], 0, 1, M, 1, 1, 0, 0, 0, 0, 0)
+        add_conv(plan, x=ptr(a), x_cs=a_cs, x_co=a_co, B=1, Hi=1, Wi=M, cin_p=spec.cin_p, Hg=1, Wg=M, in_s=1,
+                 taps=[(0, 0)], wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
+                 out=ptr(out), out_cs=out.shape[-1], out_co=0, Ho=1, Wo=M, cin=spec.cin, cout=spec.cout,
+                 tag="gcn_gemm")
 
     def off(t, floats):
         return ptr(t) if floats == 0 else type(ptr(t))(t.data_ptr() + 4 * floats)

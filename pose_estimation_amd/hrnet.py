@@ -28,7 +28,7 @@ import torch.nn as nn
 from . import ops
 from .config import load_hrnet_spec
 from .ops import Act, pad4
-from .runtime import Plan, ptr
+from .runtime import Plan, add_conv, ptr
 
 BN_MOMENTUM = 0.1
 
@@ -210,20 +210,19 @@ class _Builder:
         self.emit_conv(x, spec, out, res, relu)
         return out
 
-    def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool):
+    def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         np_ = pad4(spec.cout)
         for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off)):
             if spec.kind == "conv":
                 Hg, Wg, in_s, osy, osx = out.H, out.W, spec.stride, 1, 1
             else:
                 Hg, Wg, in_s, osy, osx = x.H, x.W, 1, 2, 2
-            self.plan.add("krrn_conv2d_f32",
-                          ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, Hg, Wg, in_s, len(taps),
-                          ops._int_array([t[0] for t in taps]), ops._int_array([t[1] for t in taps]),
-                          ptr(spec.wt[cls]), np_, np_, ptr(spec.scale), ptr(spec.bias), ptr(None), 1,
-                          ptr(res.t if res is not None else None), res.cs if res is not None else 0,
-                          res.co if res is not None else 0, ptr(out.t), out.cs, out.co, out.H, out.W,
-                          osy, osx, ooy, oox, int(relu), 0, 0)
+            add_conv(self.plan, x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=Hg,
+                     Wg=Wg, in_s=in_s, taps=taps, wt=ptr(spec.wt[cls]), N=np_, n_store=np_, scale=ptr(spec.scale),
+                     bias=ptr(spec.bias), res=ptr(res.t) if res is not None else None,
+                     res_cs=res.cs if res is not None else 0, res_co=res.co if res is not None else 0,
+                     out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=osy, osx=osx, ooy=ooy,
+                     oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag)
 
     def resize(self, x: Act, out: Act, add: Optional[Act] = None, align: bool = False, relu: bool = False):
         assert x.cp == out.cp

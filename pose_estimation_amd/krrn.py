@@ -33,7 +33,7 @@ from .fusion import FusionNetLite, build_fusion_plan, level_sizes
 from .hrnet import _Builder, build_hrnet, build_hrnet_plan
 from .ops import Act, pad4
 from .posenet import PoseNet, build_tbase_plan
-from .runtime import Late, Plan, ptr
+from .runtime import Late, Plan, add_conv, ptr
 
 
 class KRRNPlan:
@@ -108,12 +108,11 @@ class KRRNPlan:
         self.env = {"cls": self.cls, "cloud": self.cloud}
 
     def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):
-        taps = spec.taps[0]
         B, Cx, Ho, Wo = out.shape
-        self.plan.add("krrn_conv2d_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, Ho, Wo, spec.stride,
-                      len(taps), ops._int_array([t[0] for t in taps]), ops._int_array([t[1] for t in taps]),
-                      ptr(spec.wt[0]), pad4(spec.cout), n_store, ptr(spec.scale), ptr(spec.bias), ptr(None), 1,
-                      ptr(None), 0, 0, ptr(out), Cx, 0, Ho, Wo, 1, 1, 0, 0, 0, 1, 0)
+        add_conv(self.plan, x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=Ho, Wg=Wo,
+                 in_s=spec.stride, taps=spec.taps[0], wt=ptr(spec.wt[0]), N=pad4(spec.cout), n_store=n_store,
+                 scale=ptr(spec.scale), bias=ptr(spec.bias), out=ptr(out), out_cs=Cx, out_co=0, Ho=Ho, Wo=Wo,
+                 nchw=True, cin=spec.cin, cout=n_store, tag="head_final")
 
     # ------------------------------------------------------------------------------------
     def load_inputs(self, x, p_emb, choose, cls):

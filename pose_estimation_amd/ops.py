@@ -82,6 +82,7 @@ class ConvSpec:
     kind: str        # "conv" | "convT"
     ksize: int
     pad: int
+    cin: int = 0     # logical input channels (algorithmic FLOP count)
 
 
 def conv_out_hw(spec: ConvSpec, H: int, W: int) -> Tuple[int, int]:
@@ -194,7 +195,7 @@ def make_conv(conv: torch.nn.Conv2d, bn: Optional[torch.nn.Module], device, cin_
     wt = _pack_taps(w, taps_k, cin_map, cin_p, cout).to(device)
     scale, bias = fold_bn(cout, conv.bias, bn, device)
     taps = [(ky - pad, kx - pad) for (ky, kx) in taps_k]
-    return ConvSpec([wt], [taps], [(0, 0)], scale, bias, cin_p, cout, s, "conv", k, pad)
+    return ConvSpec([wt], [taps], [(0, 0)], scale, bias, cin_p, cout, s, "conv", k, pad, len(cin_map))
 
 
 def make_convT(convT: torch.nn.ConvTranspose2d, bn: Optional[torch.nn.Module], device,
@@ -229,7 +230,7 @@ def make_convT(convT: torch.nn.ConvTranspose2d, bn: Optional[torch.nn.Module], d
             taps_all.append(taps)
             offs.append((py, px))
     scale, bias = fold_bn(cout, convT.bias, bn, device)
-    return ConvSpec(wts, taps_all, offs, scale, bias, cin_p, cout, 1, "convT", kh, pad)
+    return ConvSpec(wts, taps_all, offs, scale, bias, cin_p, cout, 1, "convT", kh, pad, len(cin_map))
 
 
 def make_linear(weight: torch.Tensor, bias: Optional[torch.Tensor], bn: Optional[torch.nn.Module], device,
@@ -244,4 +245,4 @@ def make_linear(weight: torch.Tensor, bias: Optional[torch.Tensor], bn: Optional
     cin_p = pad4(max(cin_map) + 1) if cin_p is None else cin_p
     wt = _pack_taps(w[:, :, None, None], [(0, 0)], cin_map, cin_p, cout).to(device)
     scale, bias_f = fold_bn(cout, bias, bn, device)
-    return ConvSpec([wt], [[(0, 0)]], [(0, 0)], scale, bias_f, cin_p, cout, 1, "conv", 1, 0)
+    return ConvSpec([wt], [[(0, 0)]], [(0, 0)], scale, bias_f, cin_p, cout, 1, "conv", 1, 0, len(cin_map))

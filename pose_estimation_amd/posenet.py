@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .runtime import Late, Plan, ptr
+from .runtime import Late, Plan, add_conv, ptr
 
 
 class TBase(nn.Module):
@@ -64,9 +64,10 @@ def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, 
 
     def gemm(a, K, spec, out, bias2=None):
         np_ = ops.pad4(spec.cout)
-        plan.add("krrn_conv2d_f32", ptr(a), K, 0, 1, 1, M, spec.cin_p, 1, M, 1, 1, ops._int_array([0]),
-                 ops._int_array([0]), ptr(spec.wt[0]), np_, np_, ptr(spec.scale), ptr(spec.bias), ptr(bias2), N,
-                 ptr(None), 0, 0, ptr(out), out.shape[-1], 0, 1, M, 1, 1, 0, 0, 1, 0, 0)
+        add_conv(plan, x=ptr(a), x_cs=K, x_co=0, B=1, Hi=1, Wi=M, cin_p=spec.cin_p, Hg=1, Wg=M, in_s=1, taps=[(0, 0)],
+                 wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
+                 bias2=ptr(bias2) if bias2 is not None else None, b2_div=N, out=ptr(out), out_cs=out.shape[-1],
+                 out_co=0, Ho=1, Wo=M, relu=True, cin=spec.cin, cout=spec.cout, tag="tbase_gemm")
 
     gemm(feat, inc_r, spec1, h1, bias2=b2)
     gemm(h1, 1024, spec2, h2)

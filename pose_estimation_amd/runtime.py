@@ -55,13 +55,16 @@ class Late:
 
 
 class Op:
-    __slots__ = ("name", "fn", "args", "patches")
+    """One C-ABI call. `meta` carries accounting for the bench: the device kernel it launches
+    ('kernel'), algorithmic FLOPs ('flops') and compulsory HBM bytes ('bytes')."""
+    __slots__ = ("name", "fn", "args", "patches", "meta")
 
-    def __init__(self, name: str, args: Sequence[Any]):
+    def __init__(self, name: str, args: Sequence[Any], meta: Optional[dict] = None):
         self.name = name
         self.fn = getattr(_lib.lib(), name)
         self.args = list(args)
         self.patches: List[Tuple[int, str]] = [(i, a.key) for i, a in enumerate(self.args) if isinstance(a, Late)]
+        self.meta = meta or {}
 
     def __call__(self, env: Dict[str, Any]):
         args = self.args
@@ -86,8 +89,8 @@ class Plan:
         self.buffers.append(t)
         return t
 
-    def add(self, name: str, *args):
-        self.ops.append(Op(name, list(args) + [Late(STREAM)]))
+    def add(self, name: str, *args, meta: Optional[dict] = None):
+        self.ops.append(Op(name, list(args) + [Late(STREAM)], meta))
 
     def run(self, env: Dict[str, Any]):
         env[STREAM] = P(torch.cuda.current_stream(self.device).cuda_stream)
@@ -96,3 +99,56 @@ class Plan:
 
     def __len__(self):
         return len(self.ops)
+
+    def run_timed(self, env: Dict[str, Any]) -> List[float]:
+        """Run once with a HIP event pair around every launch (on the launch stream);
+        returns per-op device milliseconds. Diagnostic only (events serialise nothing, but the
+        host-side recording makes this slower than a plain/graph run)."""
+        stream = torch.cuda.current_stream(self.device)
+        env[STREAM] = P(stream.cuda_stream)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(self.ops) + 1)]
+        evs[0].record(stream)
+        for i, op in enumerate(self.ops):
+            op(env)
+            evs[i + 1].record(stream)
+        stream.synchronize()
+        return [evs[i].elapsed_time(evs[i + 1]) for i in range(len(self.ops))]
+
+
+def conv_tile(M: int, N: int) -> int:
+    """Tile choice for krrn_conv2d_f32 (1 = 128x128, 2 = 128x64, 3 = 64x64): the largest tile
+    that still puts >= 2 workgroups on each of the 256 CUs."""
+    cd = lambda a, b: (a + b - 1) // b  # noqa: E731
+    if N > 64 and cd(M, 128) * cd(N, 128) >= 512:
+        return 1
+    if cd(M, 128) * cd(N, 64) >= 512:
+        return 2
+    return 3
+
+
+CONV_KERNELS = {1: "conv_gemm_f32<128,128>", 2: "conv_gemm_f32<128,64>", 3: "conv_gemm_f32<64,64>"}
+
+
+def _iarr(vals):
+    arr = (ctypes.c_int * 9)()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
+    return arr
+
+
+def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_store, scale, bias,
+             bias2=None, b2_div=1, res=None, res_cs=0, res_co=0, out, out_cs, out_co, Ho, Wo, osy=1, osx=1, ooy=0,
+             oox=0, relu=False, nchw=False, cin=None, cout=None, tag="", tile=None):
+    """Append one krrn_conv2d_f32 launch. Pointers are ctypes values (see `ptr`). cin/cout are the
+    logical channel counts used for the algorithmic FLOP count 2*cin*cout*ntaps*M."""
+    M = B * Hg * Wg
+    tile = conv_tile(M, N) if tile is None else tile
+    cin = cin_p if cin is None else cin
+    cout = n_store if cout is None else cout
+    flops = 2.0 * cin * cout * len(taps) * M
+    plan.add("krrn_conv2d_f32", x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, len(taps), _iarr([t[0] for t in taps]),
+             _iarr([t[1] for t in taps]), wt, N, n_store, scale, bias, bias2 if bias2 is not None else P(0), b2_div,
+             res if res is not None else P(0), res_cs, res_co, out, out_cs, out_co, Ho, Wo, osy, osx, ooy, oox,
+             int(relu), int(nchw), tile,
+             meta=dict(kernel=CONV_KERNELS[tile] + (",nchw" if nchw else ""), flops=flops, tag=tag, M=M, N=N,
+                       K=cin_p * len(taps)))
