@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from pose_estimation_amd import distributed as kd  # noqa: E402
 from pose_estimation_amd.config import make_config  # noqa: E402
 from pose_estimation_amd.krrn import KRRN  # noqa: E402
 from pose_estimation_amd.pose import add_pose_ops  # noqa: E402
@@ -63,13 +64,6 @@ class Step:
         self.kp.run()
         self.pose_plan.run({})
 
-    def pack_record(self):
-        B = self.record.shape[0]
-        self.record[:, 0:9].copy_(self.R.view(B, 9))
-        self.record[:, 9:12].copy_(self.t)
-        self.record[:, 12:15].copy_(self.kp.pred_t)
-        self.record[:, 15].copy_(self.inl)
-
     def profile(self):
         """Per-op device time (HIP events around every launch, eager) -> list of (op, ms)."""
         out = []
@@ -98,9 +92,11 @@ def roofline_from_profile(prof, B: int):
     breakdown = {k: {"ms": round(v["ms"], 4), "launches": v["n"],
                      **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {})}
                  for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])}
+    traffic, tsrc = _pmc_traffic(dom)
     roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
             "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4) if achieved else None, "traffic": None,
+            "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4) if achieved else None, "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
             "launches": g["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
             "flops_per_launch": round(g["flops"] / g["n"]),
             "all_conv_gemm": {"ms_per_step": round(conv_ms, 3),
@@ -108,6 +104,21 @@ def roofline_from_profile(prof, B: int):
                               "GFLOP_per_crop": round(conv_fl / B / 1e9, 3)},
             "events_ms_per_step": round(total_ms, 3)}
     return roof, breakdown
+
+
+def _pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
+    same bench command (profiles/r*_pmc_traffic.json, built by profiles/pmc_traffic.py with the
+    gfx950 FETCH_SIZE x2 correction). None when no summary exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    if kernel not in d:
+        return None, None
+    return round(d[kernel]["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(B: int, S: int, N: int, backbone: str, budget_s: float):
@@ -159,12 +170,7 @@ def main():
     ap.add_argument("--breakdown", default="", help="write the per-kernel breakdown JSON here")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, world, local = kd.init_from_env("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     B, S, N = args.batch, args.size, args.points
@@ -177,7 +183,6 @@ def main():
     data = make_batch(B, S, N, seed=1 + rank)
     step = Step(model, data, B, S, N, dev)
     step.kp.seed.fill_(1000003 * (rank + 1))
-    gather_buf = torch.zeros((world * B, 16), dtype=torch.float32, device=dev) if world > 1 else None
 
     step.run()  # eager warm-up (compiles nothing; touches every buffer)
     torch.cuda.synchronize()
@@ -200,8 +205,8 @@ def main():
         else:
             step.run()
         if world > 1:
-            step.pack_record()
-            dist.all_gather_into_tensor(gather_buf, step.record)
+            kd.pack_records(step.R, step.t, step.kp.pred_t, step.inl, out=step.record)
+            kd.gather_records(step.record)
 
     for _ in range(args.warmup):
         one_step()

@@ -1,0 +1,151 @@
+/*
+ * krrn_hip.h — C ABI of libkrrn_hip.so, the MI355X (gfx950) kernels of the KRRN dense-fusion
+ * inference path of yaomy533/pose_estimation (lib/network/krrn.py + tools/trainer.py:383-438).
+ *
+ * The reference has no FFI (pure Python/PyTorch); each entry point below names
+ * the reference function(s) whose arithmetic it replaces. The Python host side
+ * (pose_estimation_amd/) keeps the reference's model/loader/get_pose API and binds these
+ * symbols with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Contract shared by every entry point
+ *   - Ownership: the caller allocates every input, output and workspace buffer (device
+ *     memory); the library never allocates, keeps no global state and is reentrant.
+ *   - Streams: all work is enqueued on `stream` (a hipStream_t); no host synchronisation, so
+ *     every call can be captured into a hipGraph.
+ *   - Errors: 0 = launched; KRRN_EARG (-1) null pointer / bad enum, KRRN_ESHAPE (-2) size out
+ *     of range, KRRN_EALIGN (-3) 16-byte / channel-multiple-of-4 violation — all detected on
+ *     the host before any launch; a positive value is the hipError_t of the launch.
+ *   - Layouts: activations are NHWC f32 with a channel stride `*_cs` and channel offset
+ *     `*_co` (so a buffer can be a slice of a concat); point sets are [B][n][stride] f32 with a
+ *     batch stride `*_bs` (floats); indices produced by the library are int32.
+ */
+#ifndef KRRN_HIP_H
+#define KRRN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KRRN_OK 0
+#define KRRN_EARG (-1)
+#define KRRN_ESHAPE (-2)
+#define KRRN_EALIGN (-3)
+
+/* Implicit-GEMM convolution / GEMM on the f32 matrix cores, BN folded into scale/bias.
+ * Replaces nn.Conv2d + BatchNorm2d (+ residual add) (+ ReLU) of BasicBlock / Bottleneck /
+ * transitions / fuse layers / last_layer (lib/network/hrnet/myhrnet.py:34-103, 177-221,
+ * 328-381), the XYZNet / NMLNet convs and 1x1 heads (lib/network/krrn.py:46-84),
+ * ConvTranspose2d (myhrnet.py:314-326, krrn.py:47) as 4 parity-class launches, the GCN
+ * `feature_map @ weights + bias` (lib/network/point/gcn3d.py:151, 203) and the TBase Conv1d
+ * chain (lib/network/pose/posenet.py:58-77).
+ *   out[m, n] = act(scale[n] * sum_k A[m,k] W[n,k] + bias[n] + bias2[m / b2_div, n] + res[m, n])
+ *   m = (b, gy, gx) on a B x Hg x Wg grid; k = (tap, c), A = in[b, gy*in_s + tap_dy, gx*in_s + tap_dx, c]
+ *   output pixel (gy*osy + ooy, gx*osx + oox) of a Ho x Wo map; wt is [N][ntaps*cin] row-major.
+ *   N = computed channels (multiple of 4), n_store <= N stored; out_nchw = 1 writes
+ *   out[b][out_co + n][oy][ox] with out_cs = total channels. tile: 0 auto, 1 = 128x128,
+ *   2 = 128x64, 3 = 64x64. */
+int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin, int Hg, int Wg,
+                    int in_s, int ntaps, const int* tap_dy, const int* tap_dx, const float* wt, int N,
+                    int n_store, const float* scale, const float* bias, const float* bias2, int b2_div,
+                    const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co, int Ho,
+                    int Wo, int osy, int osx, int ooy, int oox, int relu, int out_nchw, int tile, void* stream);
+
+/* k nearest neighbours without the [n, n] distance matrix.
+ * Replaces gcn3d.get_neighbor_index (gcn3d.py:15-26; mode 0, drop_first = 1: topk(k+1)[1:])
+ * and gcn3d.get_nearest_index (gcn3d.py:29-38; mode 1, k = 1, drop_first = 0).
+ * Queries: q + b*q_bs + qi*q_st (qi = qidx[t] if qidx else t, t < nq; qidx shared by the
+ * batch: the Pool_layer randperm rows, gcn3d.py:239); candidates c + b*c_bs + j*c_st, j < nc;
+ * d = 3 or 9. Exact f32 expression order (no FMA):
+ *   mode 0: ((-2 <q,c>) + |c|^2) + |q|^2      mode 1: (|c|^2 + |q|^2) - 2 <q,c>
+ * with <.,.> and |.|^2 summed sequentially over d; ties -> lower index.
+ * out: int32 [B][nq][k]. k + drop_first <= 16. */
+int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, const int* qidx, const float* c,
+                 long long c_bs, int c_st, int nc, int d, int k, int drop_first, int mode, int B, int* out,
+                 void* stream);
+
+/* 3D-GCN neighbourhood reduction, fused with the BN1d + ReLU FusionNetLite applies.
+ * Y == NULL: Conv_surface (gcn3d.py:88-112):  out[i,c] = sum_s max_j relu(dir_ij . dn[:, sC+c])
+ * Y != NULL: Conv_layer / Conv_fuse_layer (gcn3d.py:136-216):
+ *   out[i,c] = Y[i,c] + sum_s max_j relu(dir_ij . dn[:, sC+c]) * Y[idx[i,j], C + sC + c]
+ * then out = out*bn_scale + bn_bias (if given), relu (if set) (fusion.py:183-213).
+ * dir_ij = F.normalize(v[idx[i,j]] - v[i]) over d = 3 or 9 coords (v stride v_st);
+ * dn = F.normalize(directions, dim=0) [d][S*C]; Y [B][n][(S+1)*C]; idx int32 [B][n][k], k <= 16;
+ * out + b*o_bs + i*o_st + c. */
+int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, long long v_bs, int v_st, int d,
+                      const float* dn, int S, int C, const float* Y, const float* bn_scale, const float* bn_bias,
+                      int relu, float* out, long long o_bs, int o_st, int B, void* stream);
+
+/* Pool_layer max (gcn3d.py:233-236) at the sampled rows only: out[b,t,:] = max_j F[b, nbr[b,t,j], :].
+ * C, strides multiple of 4 (float4). */
+int krrn_pool_max_f32(const int* nbr, int nq, int kk, const float* F, long long f_bs, int f_st, int C, float* out,
+                      long long o_bs, int o_st, int B, void* stream);
+
+/* Bilinear resize NHWC (F.interpolate(mode='bilinear'), myhrnet.py:242-245 / 511-516 with
+ * align_corners = 0; nn.UpsamplingBilinear2d, krrn.py:56/78, with align_corners = 1), optionally
+ * out = add + resize(in) and ReLU: the HRNet fuse-layer "y = y + interpolate(...)" step. */
+int krrn_resize_bilinear_f32(const float* in, int B, int Hi, int Wi, int in_cs, int in_co, int C, float* out,
+                             int Ho, int Wo, int out_cs, int out_co, const float* add, int add_cs, int add_co,
+                             int align_corners, int relu, void* stream);
+
+/* out = relu?(a + b) on NHWC channel slices (HRNet fuse identity term, myhrnet.py:237-238;
+ * b == NULL copies a, the concat of myhrnet.py:516). */
+int krrn_add_relu_f32(const float* a, int a_cs, int a_co, const float* b, int b_cs, int b_co, float* out,
+                      int o_cs, int o_co, long long npix, int C, int relu, void* stream);
+
+/* NCHW [B][C][H][W] -> NHWC channel slice (the API boundary of KRRN.forward's x). */
+int krrn_nchw_to_nhwc_f32(const float* in, int B, int C, int H, int W, float* out, int o_cs, int o_co,
+                          void* stream);
+
+/* Per-crop class selection of the xyz / normal maps + F.normalize(p=2, dim=1, eps=1e-12)
+ * (krrn.py:105-108). fx: xyz_final output NCHW [B][Cx][H][W] (xyz block at channel xyz_off),
+ * fn: nml_final output [B][Cn][H][W]; cls int64 [B]. */
+int krrn_heads_select_f32(const float* fx, int Cx, int xyz_off, const float* fn, int Cn, const long long* cls,
+                          float* xyz_out, float* nml_out, int B, int H, int W, void* stream);
+
+/* The `choose` gather (krrn.py:121-122) packed as P9 [B][N][9] = [cloud | xyz_emb | nml_emb]
+ * (the feat_feature layout of fusion.py:194). choose int64 [B][N]. */
+int krrn_points_gather_f32(const float* cloud, const float* xyz, const float* nml, const long long* choose, int B,
+                           int N, int H, int W, float* p9, void* stream);
+
+/* Row gather dst[b, r, 0:width] = src[b, idx[b*idx_bs + r], 0:width] (int32 or int64 idx;
+ * idx_bs = 0 shares one index list across the batch): Pool_layer sampling (gcn3d.py:240-241),
+ * indexing_neighbor by the nearest indices into the 1280-wide concat (fusion.py:234-238),
+ * the one-hot column of TBase conv1 (krrn.py:132-138). */
+int krrn_gather_rows_f32(const void* idx, int idx64, long long idx_bs, int nrows, const float* src, long long src_bs,
+                         int src_st, float* dst, long long dst_bs, int dst_st, int width, int B, void* stream);
+
+/* TBase conv4 (first 3 outputs, posenet.py:76-80) + pred_t = mean_N(cloud + t_res) (krrn.py:153).
+ * h [B][n][C]; w4 [3][C]; b4 [3]; cloud [B][n][3]; pred_t [B][3]; t_res optional [B][n][3]. */
+int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const float* w4, const float* b4, const float* cloud,
+                        float* pred_t, float* t_res, void* stream);
+
+/* Batched PnP-RANSAC: Trainer.get_pose (tools/trainer.py:383-438), cv2.solvePnPRansac(EPNP,
+ * reprojectionError = thr, confidence 0.9999) restated: one workgroup per crop.
+ * xyz [B][3][HW] (normalised model coords), choose int64 [B][N], sel int32 [B][P] (the
+ * randperm(N)[:P] subset), x/ymap [B][N] full-frame pixels, K4 [B][4] = fx fy cx cy,
+ * extent / lfborder f64 [B][3], subsets int32 [B][H][5]. Outputs R [B][9] row-major, t [B][3],
+ * inlier count [B] (0 = RANSAC failed -> R = I, t = 0), inlier_mask [B][P] (optional). */
+int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choose, int N, const int* sel, int P,
+                        const float* xmap, const float* ymap, const float* K4, const double* extent,
+                        const double* lfborder, const int* subsets, int H, float thr, float* R, float* t,
+                        int* inliers, unsigned char* inlier_mask, int B, void* stream);
+
+/* torch.randperm(n)[:k] per row (gcn3d.py:239, trainer.py:407) from a counter-based generator
+ * seeded by *seed_ptr (device memory) and `stream_id`; n <= 4096. out int32 [rows][k]. */
+int krrn_randperm_i32(const unsigned long long* seed_ptr, unsigned int stream_id, int n, int k, int rows, int* out,
+                      void* stream);
+
+/* RANSAC subsets: 5 distinct indices in [0, P) per (crop, hypothesis); out int32 [B][H][5]. */
+int krrn_ransac_subsets(const unsigned long long* seed_ptr, unsigned int stream_id, int B, int H, int P, int* out,
+                        void* stream);
+
+/* *seed_ptr += 1 (last node of a replayed step). */
+int krrn_rng_advance(unsigned long long* seed_ptr, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KRRN_HIP_H */

@@ -111,22 +111,24 @@ static void lsq_solve(const double* A, int m, int n, const double* b, double* x)
   }
 }
 
-/* 3x3 inverse via the adjugate (CC is well conditioned by construction: PCA axes) */
-static int inv3(const double* a, double* r) {
-  const double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) +
-                     a[2] * (a[3] * a[7] - a[4] * a[6]);
-  if (fabs(det) < 1e-300) return 0;
-  const double id = 1.0 / det;
-  r[0] = (a[4] * a[8] - a[5] * a[7]) * id;
-  r[1] = (a[2] * a[7] - a[1] * a[8]) * id;
-  r[2] = (a[1] * a[5] - a[2] * a[4]) * id;
-  r[3] = (a[5] * a[6] - a[3] * a[8]) * id;
-  r[4] = (a[0] * a[8] - a[2] * a[6]) * id;
-  r[5] = (a[2] * a[3] - a[0] * a[5]) * id;
-  r[6] = (a[3] * a[7] - a[4] * a[6]) * id;
-  r[7] = (a[1] * a[6] - a[0] * a[7]) * id;
-  r[8] = (a[0] * a[4] - a[1] * a[3]) * id;
-  return 1;
+/* 3x3 pseudo-inverse (OpenCV inverts CC with CV_SVD): for planar point sets the third PCA
+ * axis has zero length, CC is singular and the pseudo-inverse gives the 4th control point a
+ * zero barycentric weight, which is how EPnP handles the planar case.
+ * a^+ = sum_{w_i > tol} (1 / w_i) v_i v_i^T a^T with (w, v) = eig(a^T a). */
+static void pinv3(const double* a, double* r) {
+  double AtA[9], w[3], V[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) AtA[i * 3 + j] = a[0 * 3 + i] * a[0 * 3 + j] + a[1 * 3 + i] * a[1 * 3 + j] + a[2 * 3 + i] * a[2 * 3 + j];
+  jacobi_eig(AtA, 3, w, V);
+  const double tol = (w[0] > 0 ? w[0] : 0.0) * 1e-20;
+  double P[9] = {0};
+  for (int k = 0; k < 3; ++k) {
+    if (w[k] <= tol) continue;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) P[i * 3 + j] += V[k * 3 + i] * V[k * 3 + j] / w[k];
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) r[i * 3 + j] = P[i * 3 + 0] * a[j * 3 + 0] + P[i * 3 + 1] * a[j * 3 + 1] + P[i * 3 + 2] * a[j * 3 + 2];
 }
 
 /* Procrustes: R, t minimising sum ||R pw + t - pc||^2 (Kabsch). */
@@ -201,7 +203,7 @@ static void ctrl_points(const double* pw, int n, double cws[4][3], double ccinv[
   double CC[9];
   for (int i = 0; i < 3; ++i)
     for (int j = 1; j < 4; ++j) CC[i * 3 + j - 1] = cws[j][i] - cws[0][i];
-  if (!inv3(CC, ccinv)) memset(ccinv, 0, sizeof(double) * 9);
+  pinv3(CC, ccinv);
 }
 
 static void alphas_of(const double* p, double cws[4][3], const double* ci, double a[4]) {

@@ -9,10 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define KRRN_OK 0
-#define KRRN_EARG -1      // null pointer / bad enum
-#define KRRN_ESHAPE -2    // dimension out of supported range
-#define KRRN_EALIGN -3    // float4 alignment / channel-stride violation
+// the public declarations: every definition below must match them (checked by the compiler)
+#include "../../include/krrn_hip.h"
 
 #define KRRN_API extern "C" __attribute__((visibility("default")))
 

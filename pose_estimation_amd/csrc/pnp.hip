@@ -105,21 +105,22 @@ __device__ void lsq_solve(const double* A, int m, int n, const double* b, double
   }
 }
 
-__device__ bool inv3(const double* a, double* r) {
-  const double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) +
-                     a[2] * (a[3] * a[7] - a[4] * a[6]);
-  if (fabs(det) < 1e-300) return false;
-  const double id = 1.0 / det;
-  r[0] = (a[4] * a[8] - a[5] * a[7]) * id;
-  r[1] = (a[2] * a[7] - a[1] * a[8]) * id;
-  r[2] = (a[1] * a[5] - a[2] * a[4]) * id;
-  r[3] = (a[5] * a[6] - a[3] * a[8]) * id;
-  r[4] = (a[0] * a[8] - a[2] * a[6]) * id;
-  r[5] = (a[2] * a[3] - a[0] * a[5]) * id;
-  r[6] = (a[3] * a[7] - a[4] * a[6]) * id;
-  r[7] = (a[1] * a[6] - a[0] * a[7]) * id;
-  r[8] = (a[0] * a[4] - a[1] * a[3]) * id;
-  return true;
+// 3x3 pseudo-inverse (OpenCV inverts CC with CV_SVD): planar point sets make CC singular and
+// the pseudo-inverse gives the 4th control point zero weight (EPnP's planar case).
+__device__ void pinv3(const double* a, double* r) {
+  double AtA[9], w[3], V[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) AtA[i * 3 + j] = a[i] * a[j] + a[3 + i] * a[3 + j] + a[6 + i] * a[6 + j];
+  jacobi_eig(AtA, 3, w, V);
+  const double tol = (w[0] > 0 ? w[0] : 0.0) * 1e-20;
+  double P[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < 3; ++k) {
+    if (w[k] <= tol) continue;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) P[i * 3 + j] += V[k * 3 + i] * V[k * 3 + j] / w[k];
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) r[i * 3 + j] = P[i * 3] * a[j * 3] + P[i * 3 + 1] * a[j * 3 + 1] + P[i * 3 + 2] * a[j * 3 + 2];
 }
 
 __device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
@@ -287,8 +288,7 @@ __device__ void epnp(const Pts& P, const Cam& cam, double* Rout, double* tout) {
     double CC[9];
     for (int i = 0; i < 3; ++i)
       for (int j = 1; j < 4; ++j) CC[i * 3 + j - 1] = cws[j][i] - cws[0][i];
-    if (!inv3(CC, ci))
-      for (int i = 0; i < 9; ++i) ci[i] = 0.0;
+    pinv3(CC, ci);
   }
   double MtM[144];
   for (int i = 0; i < 144; ++i) MtM[i] = 0.0;
