@@ -125,12 +125,14 @@ int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const float* w4, co
  * reprojectionError = thr, confidence 0.9999) restated: one workgroup per crop.
  * xyz [B][3][HW] (normalised model coords), choose int64 [B][N], sel int32 [B][P] (the
  * randperm(N)[:P] subset), x/ymap [B][N] full-frame pixels, K4 [B][4] = fx fy cx cy,
- * extent / lfborder f64 [B][3], subsets int32 [B][H][5]. Outputs R [B][9] row-major, t [B][3],
- * inlier count [B] (0 = RANSAC failed -> R = I, t = 0), inlier_mask [B][P] (optional). */
+ * extent / lfborder f64 [B][3], subsets int32 [B][H][5]; workspace: B*H*13 floats (per-hypothesis
+ * pose + inlier count). Outputs R [B][9] row-major, t [B][3], inlier count [B] (0 = RANSAC failed
+ * -> R = I, t = 0), inlier_mask [B][P] (optional). Two launches: hypotheses spread over
+ * (crop, 16-hypothesis) workgroups, then one wave per crop for selection + EPnP refinement. */
 int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choose, int N, const int* sel, int P,
                         const float* xmap, const float* ymap, const float* K4, const double* extent,
-                        const double* lfborder, const int* subsets, int H, float thr, float* R, float* t,
-                        int* inliers, unsigned char* inlier_mask, int B, void* stream);
+                        const double* lfborder, const int* subsets, int H, float thr, float* workspace, float* R,
+                        float* t, int* inliers, unsigned char* inlier_mask, int B, void* stream);
 
 /* torch.randperm(n)[:k] per row (gcn3d.py:239, trainer.py:407) from a counter-based generator
  * seeded by *seed_ptr (device memory) and `stream_id`; n <= 4096. out int32 [rows][k]. */

@@ -77,9 +77,10 @@ def get_pose(pred, data, num_points: int = NUM_POINTS, n_hyp: int = N_HYP, thr: 
     t = torch.empty((B, 3), dtype=torch.float32, device=dev)
     inl = torch.empty((B,), dtype=torch.int32, device=dev)
     mask = torch.empty((B, P_), dtype=torch.uint8, device=dev)
+    ws = torch.empty((B * n_hyp * 13,), dtype=torch.float32, device=dev)
     _lib.check(lib.krrn_pnp_ransac_f32(ptr(xyz), H * W, ptr(choose), N, ptr(sel), P_, ptr(xm), ptr(ym), ptr(K4),
-                                       ptr(ext), ptr(lfb), ptr(subsets), n_hyp, float(thr), ptr(R), ptr(t), ptr(inl),
-                                       ptr(mask), B, stream), "krrn_pnp_ransac_f32")
+                                       ptr(ext), ptr(lfb), ptr(subsets), n_hyp, float(thr), ptr(ws), ptr(R), ptr(t),
+                                       ptr(inl), ptr(mask), B, stream), "krrn_pnp_ransac_f32")
     if return_info:
         return R, t, {"inliers": inl, "mask": mask, "sel": sel, "subsets": subsets}
     return R, t
@@ -98,8 +99,9 @@ def add_pose_ops(plan: Plan, xyz: torch.Tensor, choose: torch.Tensor, B: int, N:
     t = plan.buf((B, 3))
     inl = plan.buf((B,), torch.int32)
     mask = plan.buf((B, P_), torch.uint8)
+    ws = plan.buf((B * n_hyp * 13,))
     plan.add("krrn_randperm_i32", ptr(seed), 5, N, P_, B, ptr(sel))
     plan.add("krrn_ransac_subsets", ptr(seed), 6, B, n_hyp, P_, ptr(subsets))
     plan.add("krrn_pnp_ransac_f32", ptr(xyz), H * W, ptr(choose), N, ptr(sel), P_, ptr(xm), ptr(ym), ptr(K4), ptr(ext),
-             ptr(lfb), ptr(subsets), n_hyp, float(thr), ptr(R), ptr(t), ptr(inl), ptr(mask), B)
+             ptr(lfb), ptr(subsets), n_hyp, float(thr), ptr(ws), ptr(R), ptr(t), ptr(inl), ptr(mask), B)
     return R, t, inl, dict(sel=sel, subsets=subsets, mask=mask)

@@ -59,9 +59,12 @@ def test_known_pose_recovery(dev):
     assert (info["inliers"].cpu().numpy() >= 200).all()
 
 
-def test_matches_oracle_same_subsets(dev):
+@pytest.mark.parametrize("noise_px,cnt_tol,pose_tol", [(0.0, 0, 1e-4), (0.4, 8, 1e-2)])
+def test_matches_oracle_same_subsets(dev, noise_px, cnt_tol, pose_tol):
+    # noise 0.4 px against a 1 px threshold puts many points on the threshold, where the f64
+    # rounding of the 5-point EPnP (GPU vs gcc) flips a few inlier decisions
     B, N, S = 16, 1000, 100
-    xyz, data, _, _ = _scene(B, N, S, 1, outlier_frac=0.3, noise_px=0.4)
+    xyz, data, _, _ = _scene(B, N, S, 1, outlier_frac=0.3, noise_px=noise_px)
     R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
     torch.cuda.synchronize()
     sel = info["sel"].cpu().long()
@@ -72,9 +75,9 @@ def test_matches_oracle_same_subsets(dev):
         obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
         img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
         Ro, to, cnt, mask, bh = opnp.pnp_ransac(obj, img, K4, subs[b].numpy(), 1.0)
-        assert abs(int(info["inliers"][b]) - cnt) <= 2, (b, int(info["inliers"][b]), cnt)
-        assert np.abs(R[b].cpu().numpy() - Ro).max() < 1e-4
-        assert np.abs(t[b].cpu().numpy() - to).max() < 1e-4
+        assert abs(int(info["inliers"][b]) - cnt) <= cnt_tol, (b, int(info["inliers"][b]), cnt)
+        assert np.abs(R[b].cpu().numpy() - Ro).max() < pose_tol
+        assert np.abs(t[b].cpu().numpy() - to).max() < pose_tol
 
 
 def test_ransac_failure_identity(dev):
