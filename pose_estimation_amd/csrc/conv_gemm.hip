@@ -1,6 +1,6 @@
 // Implicit-GEMM convolution / GEMM on the gfx950 f32 matrix cores.
 //
-// One kernel serves every dense contraction on the KRRN path (SURVEY §8a rows H1-H8,
+// One kernel family serves every dense contraction on the KRRN path (SURVEY §8a rows H1-H8,
 // D1-D2, the GCN `feature_map @ weights` of G6/G7 and the TBase Conv1d chain P1):
 //
 //   out[m, n] = act( scale[n] * sum_k A[m, k] * W[n, k] + bias[n] + bias2[m / b2_div, n]
@@ -10,9 +10,9 @@
 //   m = (b, gy, gx) over a B x Hg x Wg grid, k = (tap, c) over ntaps x cin,
 //   A[m, (tap, c)] = in[b, gy*in_s + dy[tap], gx*in_s + dx[tap], c]   (0 outside)
 // and the output pixel of grid point (gy, gx) is (gy*osy + ooy, gx*osx + oox).
-// A stride-s conv is in_s = s with taps (ky-p, kx-p); a stride-2 transposed conv is
-// four launches (one per output parity class) with in_s = 1, osy = osx = 2 and the
-// class's 1..4 taps (sub-pixel decomposition), so no zero-inserted input exists.
+// A stride-s conv is in_s = s with taps (ky-p, kx-p); a stride-2 transposed conv is four
+// launches (one per output parity class) with in_s = 1, osy = osx = 2 and the class's 1..4
+// taps (sub-pixel decomposition), so no zero-inserted input exists.
 //
 // Numerics: operands stay f32 and are multiplied on v_mfma_f32_32x32x2_f32, which is
 // bit-for-bit a k-ordered fmaf chain (cdna_hip_programming.md §3 "FP32-input MFMA").
@@ -20,13 +20,17 @@
 // eval), so this is the reference precision, not a reduced one.
 //
 // Tiling (MI355X-first):
-//   * block = 256 threads = 4 waves as 2(M) x 2(N); block tile BM x BN, BK = 16;
-//   * both LDS tiles are k-contiguous ([row][k], row pitch 20 floats): lane half h of
-//     MFMA step j reads k = 8*(j/4) + 4h + (j%4), so one ds_read_b128 feeds 4 MFMAs
-//     and the pitch 20 (5 x 16 B) makes every 16-lane ds_read_b128 group hit 16
-//     distinct 16-B bank slots (5 is odd => r*5 mod 16 is a bijection): conflict-free;
-//   * global->register staging of tile k+1 overlaps the MFMAs of tile k (double
-//     buffered LDS, one barrier per k-tile);
+//   * block = 256 threads = 4 waves laid out WGM (along M) x 4/WGM (along N); block tile
+//     BM x BN, k-tile BK (16 or 32); the tile shapes are a menu the host picks from per layer
+//     (128x128 for the wide head convs, 256x32 / 128x32 with 4 waves along M for the
+//     18/36-channel HRNet branches so the narrow N is not padded to 64);
+//   * both LDS tiles are k-contiguous ([row][k], row pitch BK+4 floats, an odd number of
+//     16-B slots) so every 16-lane ds_read_b128 group hits 16 distinct bank slots
+//     (conflict-free) and one ds_read_b128 feeds 4 MFMAs (lane half h of MFMA step j reads
+//     k = 8*(j/4) + 4h + (j%4) inside each 8-wide k group);
+//   * global -> register staging runs two k-tiles ahead (two register sets, loop unrolled
+//     by 2 so every index is static), LDS is double buffered, one barrier per k-tile, so a
+//     tile's loads have two MFMA phases to land;
 //   * blockIdx is remapped XCD-aware so tiles that share an A panel share an L2.
 // NCHW=true swaps the MFMA operands (C^T) so the lane index runs over pixels and the
 // store into an NCHW tensor is coalesced (used for the heads' final 1x1 convs, whose
@@ -34,9 +38,6 @@
 #include "krrn_common.h"
 
 namespace {
-
-constexpr int kBK = 16;
-constexpr int kPitch = 20;  // floats per LDS row (16 + 4 pad)
 
 struct ConvArgs {
   const float* in;
@@ -62,17 +63,37 @@ struct ConvArgs {
   int M;
 };
 
-template <int BM, int BN, bool NCHW>
+template <int BM, int BN, int BK, int WGM>
+struct Cfg {
+  static constexpr int WGN = 4 / WGM;
+  static constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  static constexpr int MI = WTM / 32, NI = WTN / 32;
+  static constexpr int KQ = BK / 4;             // float4 per tile row
+  static constexpr int RPP = 256 / KQ;          // rows staged per pass
+  static constexpr int AL = (BM + RPP - 1) / RPP;
+  static constexpr int BL = (BN + RPP - 1) / RPP;
+  static constexpr int PITCH = BK + 4;          // odd number of 16-B slots
+  static constexpr int A_FLOATS = BM * PITCH, B_FLOATS = BN * PITCH;
+  static_assert(MI >= 1 && NI >= 1, "wave tile must be at least 32x32");
+  static_assert(BK % 8 == 0, "BK multiple of 8");
+};
+
+template <int AL, int BL>
+struct Stage {
+  f32x4 a[AL];
+  f32x4 b[BL];
+};
+
+template <int BM, int BN, int BK, int WGM, bool NCHW>
 __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int MI = WM / 32, NI = WN / 32;
-  constexpr int AL = BM / 64, BL = BN / 64;  // float4 staged per thread
-  constexpr int A_FLOATS = BM * kPitch, B_FLOATS = BN * kPitch;
+  using C = Cfg<BM, BN, BK, WGM>;
+  constexpr int MI = C::MI, NI = C::NI, AL = C::AL, BL = C::BL, PITCH = C::PITCH;
+  constexpr int A_FLOATS = C::A_FLOATS, B_FLOATS = C::B_FLOATS;
   __shared__ __attribute__((aligned(16))) float smem[2 * (A_FLOATS + B_FLOATS)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
 
   const int n_tiles = (a.N + BN - 1) / BN;
   const int m_tiles = (a.M + BM - 1) / BM;
@@ -81,32 +102,30 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- per-thread staging geometry -------------------------------------------------
-  const int srow = tid >> 2;       // 0..63
-  const int kq = (tid & 3) * 4;    // k offset inside the tile
+  const int srow = tid / C::KQ;
+  const int kq = (tid % C::KQ) * 4;  // k offset inside the tile
   const int HWg = a.Hg * a.Wg;
   const float* a_base[AL];
   int a_iy[AL], a_ix[AL];
   bool a_ok[AL];
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
-    const int m = m0 + srow + 64 * i;
-    a_ok[i] = m < a.M;
+    const int r = srow + C::RPP * i;
+    const int m = m0 + r;
+    a_ok[i] = (r < BM) && (m < a.M);
     const int mm = a_ok[i] ? m : 0;
     const int b = mm / HWg;
-    const int r = mm - b * HWg;
-    const int gy = r / a.Wg, gx = r - (r / a.Wg) * a.Wg;
+    const int rr = mm - b * HWg;
+    const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
     a_iy[i] = gy * a.in_s;
     a_ix[i] = gx * a.in_s;
     a_base[i] = a.in + (size_t)b * a.Hi * a.Wi * a.in_cs + a.in_co;
   }
-  // (tap, c) of this thread's first k; advanced by kBK per tile
   int tap = kq / a.cin;
   int cc = kq - tap * a.cin;
-  int kk = kq;  // absolute k of this thread's staged float4
+  int kk = kq;  // absolute k of this thread's staged float4s
 
-  f32x4 ra[AL], rb[BL];
-
-  auto load_tile = [&]() {
+  auto load_tile = [&](Stage<AL, BL>& st) {
     int ddy = 0, ddx = 0;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -117,35 +136,33 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
     for (int i = 0; i < AL; ++i) {
       const int iy = a_iy[i] + ddy, ix = a_ix[i] + ddx;
       const bool ok = a_ok[i] && tap_ok && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
-      if (ok) {
-        ra[i] = *reinterpret_cast<const f32x4*>(a_base[i] + ((size_t)iy * a.Wi + ix) * a.in_cs + cc);
-      } else {
-        ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      st.a[i] = ok ? *reinterpret_cast<const f32x4*>(a_base[i] + ((size_t)iy * a.Wi + ix) * a.in_cs + cc)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int n = n0 + srow + 64 * i;
-      if (n < a.N && kk < a.K) {
-        rb[i] = *reinterpret_cast<const f32x4*>(a.wt + (size_t)n * a.K + kk);
-      } else {
-        rb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      const int r = srow + C::RPP * i;
+      const int n = n0 + r;
+      st.b[i] = (r < BN && n < a.N && kk < a.K) ? *reinterpret_cast<const f32x4*>(a.wt + (size_t)n * a.K + kk)
+                                                : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    // advance to the next k-tile
-    kk += kBK;
-    cc += kBK;
+    kk += BK;
+    cc += BK;
     while (cc >= a.cin) { cc -= a.cin; ++tap; }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](const Stage<AL, BL>& st, int buf) {
     float* As = smem + buf * (A_FLOATS + B_FLOATS);
     float* Bs = As + A_FLOATS;
 #pragma unroll
-    for (int i = 0; i < AL; ++i)
-      *reinterpret_cast<f32x4*>(As + (srow + 64 * i) * kPitch + kq) = ra[i];
+    for (int i = 0; i < AL; ++i) {
+      const int r = srow + C::RPP * i;
+      if (r < BM) *reinterpret_cast<f32x4*>(As + r * PITCH + kq) = st.a[i];
+    }
 #pragma unroll
-    for (int i = 0; i < BL; ++i)
-      *reinterpret_cast<f32x4*>(Bs + (srow + 64 * i) * kPitch + kq) = rb[i];
+    for (int i = 0; i < BL; ++i) {
+      const int r = srow + C::RPP * i;
+      if (r < BN) *reinterpret_cast<f32x4*>(Bs + r * PITCH + kq) = st.b[i];
+    }
   };
 
   f32x16 acc[MI][NI];
@@ -156,27 +173,19 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nkt = (a.K + kBK - 1) / kBK;
-  load_tile();
-  store_tile(0);
-  __syncthreads();
-
   const int frow = lane & 31, fh = lane >> 5;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nkt;
-    if (more) load_tile();
-    const float* As = smem + cur * (A_FLOATS + B_FLOATS);
+  auto compute = [&](int buf) {
+    const float* As = smem + buf * (A_FLOATS + B_FLOATS);
     const float* Bs = As + A_FLOATS;
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < BK / 8; ++g) {
       f32x4 af[MI], bf[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
-        af[i] = *reinterpret_cast<const f32x4*>(As + (wm * WM + i * 32 + frow) * kPitch + g * 8 + 4 * fh);
+        af[i] = *reinterpret_cast<const f32x4*>(As + (wm * C::WTM + i * 32 + frow) * PITCH + g * 8 + 4 * fh);
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        bf[j] = *reinterpret_cast<const f32x4*>(Bs + (wn * WN + j * 32 + frow) * kPitch + g * 8 + 4 * fh);
+        bf[j] = *reinterpret_cast<const f32x4*>(Bs + (wn * C::WTN + j * 32 + frow) * PITCH + g * 8 + 4 * fh);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -189,7 +198,24 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
           }
     }
-    if (more) store_tile(cur ^ 1);
+  };
+
+  // ---- main loop: loads two tiles ahead, LDS double-buffered, unrolled by 2 ---------------
+  const int nkt = (a.K + BK - 1) / BK;
+  Stage<AL, BL> s0, s1;
+  load_tile(s0);
+  if (nkt > 1) load_tile(s1);
+  store_tile(s0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; kt += 2) {
+    if (kt + 2 < nkt) load_tile(s0);
+    compute(0);
+    if (kt + 1 < nkt) store_tile(s1, 1);
+    __syncthreads();
+    if (kt + 1 >= nkt) break;
+    if (kt + 3 < nkt) load_tile(s1);
+    compute(1);
+    if (kt + 2 < nkt) store_tile(s0, 0);
     __syncthreads();
   }
 
@@ -200,13 +226,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       if constexpr (!NCHW) {
-        const int n = n0 + wn * WN + j * 32 + frow;
+        const int n = n0 + wn * C::WTN + j * 32 + frow;
         if (n >= a.n_store) continue;
         const float sc = a.scale ? a.scale[n] : 1.f;
         const float bi = a.bias ? a.bias[n] : 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const int m = m0 + wm * C::WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
           if (m >= a.M) continue;
           const int b = m / HWg;
           const int rr = m - b * HWg;
@@ -220,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
           a.out[pix * a.out_cs + a.out_co + n] = v;
         }
       } else {
-        const int m = m0 + wm * WM + i * 32 + frow;
+        const int m = m0 + wm * C::WTM + i * 32 + frow;
         if (m >= a.M) continue;
         const int b = m / HWg;
         const int rr = m - b * HWg;
@@ -228,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
         const int oy = gy * a.osy + a.ooy, ox = gx * a.osx + a.oox;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int n = n0 + wn * WN + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const int n = n0 + wn * C::WTN + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
           if (n >= a.n_store) continue;
           float v = acc[i][j][r] * (a.scale ? a.scale[n] : 1.f) + (a.bias ? a.bias[n] : 0.f);
           if (a.bias2) v += a.bias2[(size_t)(m / a.b2_div) * a.N + n];
@@ -239,16 +265,17 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
     }
 }
 
-template <int BM, int BN, bool NCHW>
+template <int BM, int BN, int BK, int WGM, bool NCHW>
 int launch(const ConvArgs& a, hipStream_t s) {
   const int nwg = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
-  hipLaunchKernelGGL((conv_gemm_f32_kernel<BM, BN, NCHW>), dim3(nwg), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_f32_kernel<BM, BN, BK, WGM, NCHW>), dim3(nwg), dim3(256), 0, s, a);
   return krrn_launch_status();
 }
 
 }  // namespace
 
-// C-ABI: see include/krrn_hip.h for the argument contract.
+// Tile menu (include/krrn_hip.h): 1 128x128x16, 2 128x64x16, 3 64x64x16, 4 128x128x32,
+// 5 256x32x16 (4 waves along M), 6 128x32x32 (4 waves along M), 7 128x64x32, 8 64x64x32.
 KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin,
                              int Hg, int Wg, int in_s, int ntaps, const int* tap_dy, const int* tap_dx,
                              const float* wt, int N, int n_store, const float* scale, const float* bias,
@@ -262,6 +289,7 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
   if (n_store < 1 || n_store > N) return KRRN_ESHAPE;
   if (bias2 && b2_div < 1) return KRRN_EARG;
   if (!out_nchw && out_co + n_store > out_cs) return KRRN_ESHAPE;
+  if (tile < 0 || tile > 8) return KRRN_EARG;
   const long long M = (long long)B * Hg * Wg;
   if (M > 0x7fffffffLL) return KRRN_ESHAPE;
   ConvArgs a;
@@ -274,18 +302,25 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
   a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.Ho = Ho; a.Wo = Wo;
   a.osy = osy; a.osx = osx; a.ooy = ooy; a.oox = oox; a.relu = relu; a.M = (int)M;
   hipStream_t s = (hipStream_t)stream;
-  // tile: 0 = auto, 1 = 128x128, 2 = 128x64, 3 = 64x64
   if (tile == 0) {
     const long long wg128 = (long long)krrn_cdiv(a.M, 128) * krrn_cdiv(N, 128);
-    if (N <= 64) tile = (krrn_cdiv(a.M, 128) >= 512) ? 2 : 3;
+    if (N <= 32) tile = 5;
+    else if (N <= 64) tile = (krrn_cdiv(a.M, 128) >= 512) ? 2 : 3;
     else tile = (wg128 >= 512) ? 1 : 3;
   }
   if (out_nchw) {
-    if (tile == 1) return launch<128, 128, true>(a, s);
-    if (tile == 2) return launch<128, 64, true>(a, s);
-    return launch<64, 64, true>(a, s);
+    if (tile == 1 || tile == 4) return launch<128, 128, 16, 2, true>(a, s);
+    if (tile == 2 || tile == 7) return launch<128, 64, 16, 2, true>(a, s);
+    return launch<64, 64, 16, 2, true>(a, s);
   }
-  if (tile == 1) return launch<128, 128, false>(a, s);
-  if (tile == 2) return launch<128, 64, false>(a, s);
-  return launch<64, 64, false>(a, s);
+  switch (tile) {
+    case 1: return launch<128, 128, 16, 2, false>(a, s);
+    case 2: return launch<128, 64, 16, 2, false>(a, s);
+    case 3: return launch<64, 64, 16, 2, false>(a, s);
+    case 4: return launch<128, 128, 32, 2, false>(a, s);
+    case 5: return launch<256, 32, 16, 4, false>(a, s);
+    case 6: return launch<128, 32, 32, 4, false>(a, s);
+    case 7: return launch<128, 64, 32, 2, false>(a, s);
+    default: return launch<64, 64, 32, 2, false>(a, s);
+  }
 }

@@ -115,18 +115,24 @@ class Plan:
         return [evs[i].elapsed_time(evs[i + 1]) for i in range(len(self.ops))]
 
 
-def conv_tile(M: int, N: int) -> int:
-    """Tile choice for krrn_conv2d_f32 (1 = 128x128, 2 = 128x64, 3 = 64x64): the largest tile
-    that still puts >= 2 workgroups on each of the 256 CUs."""
+def conv_tile(M: int, N: int, K: int = 1024, nchw: bool = False) -> int:
+    """Tile choice for krrn_conv2d_f32 from the measured menu (scratch/convbench.py on MI355X,
+    graph-replayed): 128x128x32 only for very large, deep GEMMs (>= 2048 tiles, K >= 512: the
+    S=120 head convs 103 TF, TBase conv1 104 TF); 128x32x32 with 4 waves along M for N <= 32
+    (HRNet branch 0: 22 vs 15 TF for 64x64); 64x64x32 otherwise (69 TF on layer1 3x3 vs 61)."""
     cd = lambda a, b: (a + b - 1) // b  # noqa: E731
-    if N > 64 and cd(M, 128) * cd(N, 128) >= 512:
-        return 1
-    if cd(M, 128) * cd(N, 64) >= 512:
-        return 2
-    return 3
+    if nchw:
+        return 1 if cd(M, 128) * cd(N, 128) >= 512 else 3
+    if N <= 32:
+        return 6
+    if N >= 128 and K >= 512 and cd(M, 128) * cd(N, 128) >= 2048:
+        return 4
+    return 8
 
 
-CONV_KERNELS = {1: "conv_gemm_f32<128,128>", 2: "conv_gemm_f32<128,64>", 3: "conv_gemm_f32<64,64>"}
+CONV_KERNELS = {1: "conv_gemm_f32<128,128,16>", 2: "conv_gemm_f32<128,64,16>", 3: "conv_gemm_f32<64,64,16>",
+                4: "conv_gemm_f32<128,128,32>", 5: "conv_gemm_f32<256,32,16>", 6: "conv_gemm_f32<128,32,32>",
+                7: "conv_gemm_f32<128,64,32>", 8: "conv_gemm_f32<64,64,32>"}
 
 
 def _iarr(vals):
@@ -142,7 +148,7 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
     """Append one krrn_conv2d_f32 launch. Pointers are ctypes values (see `ptr`). cin/cout are the
     logical channel counts used for the algorithmic FLOP count 2*cin*cout*ntaps*M."""
     M = B * Hg * Wg
-    tile = conv_tile(M, N) if tile is None else tile
+    tile = conv_tile(M, N, cin_p * len(taps), nchw) if tile is None else tile
     cin = cin_p if cin is None else cin
     cout = n_store if cout is None else cout
     flops = 2.0 * cin * cout * len(taps) * M
