@@ -44,8 +44,9 @@ extern "C" {
  *   m = (b, gy, gx) on a B x Hg x Wg grid; k = (tap, c), A = in[b, gy*in_s + tap_dy, gx*in_s + tap_dx, c]
  *   output pixel (gy*osy + ooy, gx*osx + oox) of a Ho x Wo map; wt is [N][ntaps*cin] row-major.
  *   N = computed channels (multiple of 4), n_store <= N stored; out_nchw = 1 writes
- *   out[b][out_co + n][oy][ox] with out_cs = total channels. tile: 0 auto, 1 = 128x128,
- *   2 = 128x64, 3 = 64x64. */
+ *   out[b][out_co + n][oy][ox] with out_cs = total channels. tile (BMxBNxBK): 0 auto,
+ *   1 = 128x128x16, 2 = 128x64x16, 3 = 64x64x16, 4 = 128x128x32, 5 = 256x32x16,
+ *   6 = 128x32x32, 7 = 128x64x32, 8 = 64x64x32; out_nchw supports tiles 0-3 only. */
 int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin, int Hg, int Wg,
                     int in_s, int ntaps, const int* tap_dy, const int* tap_dx, const float* wt, int N,
                     int n_store, const float* scale, const float* bias, const float* bias2, int b2_div,

@@ -139,3 +139,43 @@ def init_weights(model: torch.nn.Module, seed: int = 0) -> Dict[str, torch.Tenso
 
 def _is_bn(key: str, sd) -> bool:
     return key.rsplit(".", 1)[0] + ".running_mean" in sd
+
+
+def make_pnp_scene(B: int, N: int, S: int, seed: int, outlier_frac: float = 0.1, noise_px: float = 0.0,
+                   planar: bool = False):
+    """get_pose inputs (trainer.py:383-438) whose chosen pixels hold the exact normalised
+    model coordinates of a known pose: `xyz` [B,3,S,S], the data dict get_pose reads, and the
+    ground truth (R [B,3,3], t [B,3]). Outliers are shifted by U[-20,20] px (SURVEY §8d KAT)."""
+    rng = np.random.default_rng(seed)
+    K4 = np.array([LM_K[0, 0], LM_K[1, 1], LM_K[0, 2], LM_K[1, 2]], np.float32)
+    ext = np.array([0.067, 0.1276, 0.1175])
+    lfb = np.array([-0.0335, -0.0638, -0.0587])
+    xyz = np.zeros((B, 3, S, S), np.float32)
+    choose = np.zeros((B, 1, N), np.int64)
+    xm = np.zeros((B, N, 1), np.float32)
+    ym = np.zeros((B, N, 1), np.float32)
+    Rs, ts = [], []
+    for b in range(B):
+        R = rand_rotation(rng)
+        t = np.array([rng.uniform(-0.1, 0.1), rng.uniform(-0.1, 0.1), rng.uniform(0.7, 1.1)])
+        pix = rng.choice(S * S, N, replace=False)
+        u32 = rng.random((N, 3)).astype(np.float32)
+        if planar:
+            u32[:, 2] = 0.5
+        pw = u32.astype(np.float64) * ext + lfb
+        pc = pw @ R.T + t
+        img = np.stack([K4[0] * pc[:, 0] / pc[:, 2] + K4[2], K4[1] * pc[:, 1] / pc[:, 2] + K4[3]], 1)
+        if noise_px:
+            img += rng.normal(scale=noise_px, size=img.shape)
+        out = rng.random(N) < outlier_frac
+        img[out] += rng.uniform(-20, 20, size=(int(out.sum()), 2))
+        xyz[b].reshape(3, -1)[:, pix] = u32.T
+        choose[b, 0] = pix
+        xm[b, :, 0] = img[:, 0]
+        ym[b, :, 0] = img[:, 1]
+        Rs.append(R)
+        ts.append(t)
+    data = {"choose": torch.from_numpy(choose), "x_map_choosed": torch.from_numpy(xm),
+            "y_map_choosed": torch.from_numpy(ym), "intrinsic": torch.from_numpy(np.tile(K4, (B, 1))),
+            "extent": torch.from_numpy(np.tile(ext, (B, 1))), "lfborder": torch.from_numpy(np.tile(lfb, (B, 1)))}
+    return torch.from_numpy(xyz), data, np.stack(Rs), np.stack(ts)
