@@ -69,8 +69,7 @@ class Step:
         out = []
         for p in (self.kp.device_perm_plan, self.kp.plan, self.pose_plan):
             env = dict(self.kp.env) if p is self.kp.plan else {}
-            ms = p.run_timed(env)
-            out.extend(zip(p.ops, ms))
+            out.extend(p.run_timed(env))
         return out
 
 

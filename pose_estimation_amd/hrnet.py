@@ -248,50 +248,56 @@ class _Builder:
         return self.conv(h, blk.conv3, blk.bn3, res=res, relu=True)
 
     def hr_module(self, xs: List[Act], m: HighResolutionModule, outs: Optional[List[Optional[Act]]] = None) -> List[Act]:
+        """myhrnet.py:226-250. Branch i (and later fuse output i) runs on plan stream i: the
+        branches are independent until the fuse, and the fuse outputs are independent again."""
+        plan = self.plan
+        nb = m.num_branches
+        side = list(range(1, nb))
         ys = []
+        plan.fork(side)
         for i, x in enumerate(xs):
-            for blk in m.branches[i]:
-                x = self.basic(x, blk)
+            with plan.on_stream(i):
+                for blk in m.branches[i]:
+                    x = self.basic(x, blk)
             ys.append(x)
-        if m.num_branches == 1:
+        plan.join(side)
+        if nb == 1:
             return ys
         fused = []
-        nb = m.num_branches
+        plan.fork(side)
         for i in range(nb):
-            out = outs[i] if outs is not None and outs[i] is not None else self.act(ys[i].H, ys[i].W, ys[i].c)
-            terms = [j for j in range(nb)]
-            acc: Optional[Act] = None  # running sum lives in `out` once written
-            for idx_t, j in enumerate(terms):
-                last = idx_t == nb - 1
-                if j == i:
-                    if acc is None:
-                        acc = ys[i]  # identity term: read in place, no copy
-                    elif last:
-                        self.add_relu(acc, ys[i], out, relu=True)
-                        acc = out
-                    else:
-                        self.add_relu(acc, ys[i], out, relu=False)
-                        acc = out
-                elif j > i:
-                    seq = m.fuse_layers[i][j]
-                    low = self.conv(ys[j], seq[0], seq[1])
-                    if acc is None:
-                        self.resize(low, out, add=None, align=False, relu=last)
-                    else:
-                        self.resize(low, out, add=acc, align=False, relu=last)
-                    acc = out
-                else:
-                    chain = m.fuse_layers[i][j]
-                    h = ys[j]
-                    for k, sub in enumerate(chain):
-                        final = k == len(chain) - 1
-                        if final:
-                            h = self.conv(h, sub[0], sub[1], out=out, res=acc, relu=last)
-                        else:
-                            h = self.conv(h, sub[0], sub[1], relu=True)
-                    acc = out
-            fused.append(out)
+            with plan.on_stream(i):
+                fused.append(self._fuse_output(ys, m, i, outs[i] if outs is not None else None))
+        plan.join(side)
         return fused
+
+    def _fuse_output(self, ys: List[Act], m: HighResolutionModule, i: int, out: Optional[Act]) -> Act:
+        nb = m.num_branches
+        out = out if out is not None else self.act(ys[i].H, ys[i].W, ys[i].c)
+        acc: Optional[Act] = None  # running sum lives in `out` once written
+        for j in range(nb):
+            last = j == nb - 1
+            if j == i:
+                if acc is None:
+                    acc = ys[i]  # identity term: read in place, no copy
+                else:
+                    self.add_relu(acc, ys[i], out, relu=last)
+                    acc = out
+            elif j > i:
+                seq = m.fuse_layers[i][j]
+                low = self.conv(ys[j], seq[0], seq[1])
+                self.resize(low, out, add=acc, align=False, relu=last)
+                acc = out
+            else:
+                chain = m.fuse_layers[i][j]
+                h = ys[j]
+                for k, sub in enumerate(chain):
+                    if k == len(chain) - 1:
+                        h = self.conv(h, sub[0], sub[1], out=out, res=acc, relu=last)
+                    else:
+                        h = self.conv(h, sub[0], sub[1], relu=True)
+                acc = out
+        return out
 
 
 def build_hrnet_plan(net: HRNet, plan: Plan, x: Act) -> Tuple[Act, Act, list]:

@@ -55,6 +55,8 @@ class KRRNPlan:
         plan.add("krrn_nchw_to_nhwc_f32", ptr(self.x_in), B, 3, S, S, ptr(xa.t), 4, 0)
         xmap, ymap, specs = build_hrnet_plan(model.backbone, plan, xa)
         bld = _Builder(plan, B)
+        # the two head towers are independent until the class select: NMLNet on stream 1
+        plan.fork([1])
         # XYZNet (krrn.py:46-65): ConvT s2 + BN + ReLU, conv + BN + ReLU, x2 bilinear
         # (align_corners=True), 2 x (conv + BN + ReLU), then xyz_final (1x1 + bias)
         X = model.XYZNet
@@ -71,15 +73,17 @@ class KRRNPlan:
         self._nchw_conv(h, spec, self.fx, model.xyz_outc)
         # NMLNet (krrn.py:68-84)
         Nn = model.NMLNet
-        g = bld.conv(ymap, Nn[0], Nn[1], relu=True)
-        g = bld.conv(g, Nn[3], Nn[4], relu=True)
-        upn = bld.act(2 * g.H, 2 * g.W, g.c)
-        bld.resize(g, upn, align=True)
-        g = bld.conv(upn, Nn[7], Nn[8], relu=True)
-        self.fn = plan.buf((B, 3 * C, g.H, g.W))
-        spec_n = ops.make_conv(model.nml_final, None, device, cin_p=g.cp)
-        bld.specs.append(spec_n)
-        self._nchw_conv(g, spec_n, self.fn, 3 * C)
+        with plan.on_stream(1):
+            g = bld.conv(ymap, Nn[0], Nn[1], relu=True)
+            g = bld.conv(g, Nn[3], Nn[4], relu=True)
+            upn = bld.act(2 * g.H, 2 * g.W, g.c)
+            bld.resize(g, upn, align=True)
+            g = bld.conv(upn, Nn[7], Nn[8], relu=True)
+            self.fn = plan.buf((B, 3 * C, g.H, g.W))
+            spec_n = ops.make_conv(model.nml_final, None, device, cin_p=g.cp)
+            bld.specs.append(spec_n)
+            self._nchw_conv(g, spec_n, self.fn, 3 * C)
+        plan.join([1])
         Ho, Wo = h.H, h.W
         self.Ho, self.Wo = Ho, Wo
         # class gather + F.normalize (krrn.py:100-108)

@@ -11,6 +11,7 @@ replayed for the steady-state loop.
 from __future__ import annotations
 
 import ctypes
+from contextlib import contextmanager
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -42,6 +43,10 @@ _lib.register("krrn_rng_advance", [P, P])
 STREAM = "__stream__"
 
 
+def _skey(sid: int) -> str:
+    return STREAM if sid == 0 else f"__stream{sid}__"
+
+
 def ptr(t: Optional[torch.Tensor]) -> P:
     return P(t.data_ptr()) if t is not None else P(0)
 
@@ -57,14 +62,15 @@ class Late:
 class Op:
     """One C-ABI call. `meta` carries accounting for the bench: the device kernel it launches
     ('kernel'), algorithmic FLOPs ('flops') and compulsory HBM bytes ('bytes')."""
-    __slots__ = ("name", "fn", "args", "patches", "meta")
+    __slots__ = ("name", "fn", "args", "patches", "meta", "sid")
 
-    def __init__(self, name: str, args: Sequence[Any], meta: Optional[dict] = None):
+    def __init__(self, name: str, args: Sequence[Any], meta: Optional[dict] = None, sid: int = 0):
         self.name = name
         self.fn = getattr(_lib.lib(), name)
         self.args = list(args)
         self.patches: List[Tuple[int, str]] = [(i, a.key) for i, a in enumerate(self.args) if isinstance(a, Late)]
         self.meta = meta or {}
+        self.sid = sid
 
     def __call__(self, env: Dict[str, Any]):
         args = self.args
@@ -76,13 +82,39 @@ class Op:
             _lib.check(st, self.name)
 
 
+class Sync:
+    """Stream dependency: `dst` waits for everything enqueued on `src` so far (an event record +
+    stream wait; under hipGraph capture this becomes a graph edge)."""
+    __slots__ = ("src", "dst", "event", "name", "meta", "sid")
+
+    def __init__(self, src: int, dst: int):
+        self.src, self.dst = src, dst
+        self.event = torch.cuda.Event() if torch.cuda.is_available() else None
+        self.name, self.meta, self.sid = "sync", {}, dst
+
+    def __call__(self, env: Dict[str, Any]):
+        streams = env["__streams__"]
+        if streams is None:  # serial run
+            return
+        self.event.record(streams[self.src])
+        streams[self.dst].wait_event(self.event)
+
+
 class Plan:
-    """An ordered launch list plus the workspaces it owns."""
+    """An ordered launch list plus the workspaces it owns.
+
+    Ops are tagged with a stream id (`on_stream`); id 0 is the caller's current stream and ids
+    1.. are plan-owned side streams, ordered by explicit `fork` / `join` points. Independent
+    HRNet branches and head towers use this to run concurrently (one small conv cannot fill 256
+    CUs; four of them side by side fill more). `run(serial=True)` puts everything on stream 0."""
 
     def __init__(self, device: torch.device):
         self.device = device
-        self.ops: List[Op] = []
+        self.ops: List[Any] = []
         self.buffers: List[torch.Tensor] = []  # keep-alive
+        self.cur = 0
+        self.nstreams = 1
+        self._side: List[torch.cuda.Stream] = []
 
     def buf(self, shape, dtype=torch.float32, zero: bool = True) -> torch.Tensor:
         t = (torch.zeros if zero else torch.empty)(tuple(shape), dtype=dtype, device=self.device)
@@ -90,29 +122,63 @@ class Plan:
         return t
 
     def add(self, name: str, *args, meta: Optional[dict] = None):
-        self.ops.append(Op(name, list(args) + [Late(STREAM)], meta))
+        self.ops.append(Op(name, list(args) + [Late(_skey(self.cur))], meta, self.cur))
 
-    def run(self, env: Dict[str, Any]):
-        env[STREAM] = P(torch.cuda.current_stream(self.device).cuda_stream)
+    @contextmanager
+    def on_stream(self, sid: int):
+        prev, self.cur = self.cur, sid
+        self.nstreams = max(self.nstreams, sid + 1)
+        try:
+            yield
+        finally:
+            self.cur = prev
+
+    def fork(self, sids: Sequence[int]):
+        """Side streams `sids` wait for all work so far on stream 0."""
+        for s in sids:
+            if s != 0:
+                self.ops.append(Sync(0, s))
+
+    def join(self, sids: Sequence[int]):
+        """Stream 0 waits for all work so far on side streams `sids`."""
+        for s in sids:
+            if s != 0:
+                self.ops.append(Sync(s, 0))
+
+    def _streams(self, env: Dict[str, Any], serial: bool):
+        main = torch.cuda.current_stream(self.device)
+        while len(self._side) < self.nstreams - 1:
+            self._side.append(torch.cuda.Stream(self.device))
+        streams = [main] + self._side
+        for sid in range(self.nstreams):
+            env[_skey(sid)] = P((main if serial else streams[sid]).cuda_stream)
+        env["__streams__"] = None if serial else streams
+        return main
+
+    def run(self, env: Dict[str, Any], serial: bool = False):
+        self._streams(env, serial)
         for op in self.ops:
             op(env)
 
     def __len__(self):
         return len(self.ops)
 
-    def run_timed(self, env: Dict[str, Any]) -> List[float]:
-        """Run once with a HIP event pair around every launch (on the launch stream);
-        returns per-op device milliseconds. Diagnostic only (events serialise nothing, but the
-        host-side recording makes this slower than a plain/graph run)."""
-        stream = torch.cuda.current_stream(self.device)
-        env[STREAM] = P(stream.cuda_stream)
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(self.ops) + 1)]
+    def kernels(self) -> List[Op]:
+        return [op for op in self.ops if isinstance(op, Op)]
+
+    def run_timed(self, env: Dict[str, Any]) -> List[Tuple[Op, float]]:
+        """Run once serially with a HIP event pair around every launch (on the launch stream);
+        returns (op, device ms) per kernel launch. Diagnostic only: the host-side recording
+        makes this slower than a plain/graph run."""
+        stream = self._streams(env, serial=True)
+        kops = self.kernels()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(kops) + 1)]
         evs[0].record(stream)
-        for i, op in enumerate(self.ops):
+        for i, op in enumerate(kops):
             op(env)
             evs[i + 1].record(stream)
         stream.synchronize()
-        return [evs[i].elapsed_time(evs[i + 1]) for i in range(len(self.ops))]
+        return [(op, evs[i].elapsed_time(evs[i + 1])) for i, op in enumerate(kops)]
 
 
 def conv_tile(M: int, N: int, K: int = 1024, nchw: bool = False) -> int:
