@@ -316,11 +316,16 @@ class Pool_layer(nn.Module):  # noqa: N801
         super().__init__()
         self.pooling_rate, self.neighbor_num = pooling_rate, neighbor_num
 
-    def forward(self, v, fm, perm=None):
+    def forward(self, v, fm, perm=None, idx_override=None):
+        """idx_override (test conditioning): use these neighbour indices for the max instead of
+        the kNN result (which is still computed and kept in `last_idx`)."""
         n = v.shape[1]
         pool_num = int(n / self.pooling_rate)
         sample = torch.randperm(n)[:pool_num] if perm is None else perm[:pool_num].long()
         idx = get_neighbor_index(v[..., :3], self.neighbor_num, rows=sample)
+        self.last_idx = idx
+        if idx_override is not None:
+            idx = idx_override.long()
         pooled = torch.max(indexing_neighbor(fm, idx), dim=2)[0]
         return v[:, sample, :], pooled, sample
 
@@ -346,7 +351,8 @@ class FusionNetLite(nn.Module):
     def _bnr(bn, x):
         return F.relu(bn(x.transpose(1, 2)).transpose(1, 2))
 
-    def forward(self, vertices, xyz, normal, perms: Optional[Sequence[torch.Tensor]] = None, trace=None):
+    def forward(self, vertices, xyz, normal, perms: Optional[Sequence[torch.Tensor]] = None, trace=None,
+                pool_override=None):
         perms = list(perms) if perms is not None else [None] * 5
         k0 = self.neighbor_num
         idx0 = get_neighbor_index(vertices, k0)
@@ -359,7 +365,8 @@ class FusionNetLite(nn.Module):
         feat_feature = torch.cat([vertices, xyz, normal], 2)
         vp, fp, used = {}, {}, []
         for i, br in enumerate(("v", "x", "n")):
-            vp[br], fp[br], s = getattr(self, f"pool_1_{br}")(pts[br], fm1[br], perms[i])
+            ov = pool_override.get(br) if pool_override else None
+            vp[br], fp[br], s = getattr(self, f"pool_1_{br}")(pts[br], fm1[br], perms[i], idx_override=ov)
             used.append(s)
         pool_1, _, s = self.pool_1(feat_feature, feat_1, perms[3])
         used.append(s)
@@ -372,15 +379,18 @@ class FusionNetLite(nn.Module):
         used.append(s)
         k2 = min(k0, pool_2.shape[1] // 8)
         idx2 = get_neighbor_index(pool_2, k2)
-        fm_4 = self.conv_4(idx2, pool_2, fm_pool_2)
-        fm_5 = self.conv_5(idx2, pool_2, fm_4)
+        idx2_used = pool_override["idx2"].long() if pool_override and "idx2" in pool_override else idx2
+        fm_4 = self.conv_4(idx2_used, pool_2, fm_pool_2)
+        fm_5 = self.conv_5(idx2_used, pool_2, fm_4)
         nn1 = get_nearest_index(vertices, pool_1[..., :3])
         nn2 = get_nearest_index(vertices, pool_2[..., :3])
         feat = torch.cat([indexing_neighbor(fm_5, nn2).squeeze(2), indexing_neighbor(feat_1, nn1).squeeze(2),
                           indexing_neighbor(feat_2, nn1).squeeze(2)], 2)
         if trace is not None:
             trace.update(idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1[..., 0], nn2=nn2[..., 0], feat1=feat_1,
-                         feat2=feat_2, fm5=fm_5, pool_1=pool_1, pool_2=pool_2, perms=used)
+                         feat2=feat_2, fm5=fm_5, pool_1=pool_1, pool_2=pool_2, perms=used,
+                         pool_v=self.pool_1_v.last_idx, pool_x=self.pool_1_x.last_idx,
+                         pool_n=self.pool_1_n.last_idx, pool2=self.pool_2.last_idx)
         return feat
 
 
@@ -438,7 +448,8 @@ class KRRNOracle(nn.Module):
         self.pose = PoseNet(inc_r + C, out_t)
 
     @torch.no_grad()
-    def forward(self, x, p_emb, choose, cls, region_point=None, opt_pose=True, perms=None, trace=None):
+    def forward(self, x, p_emb, choose, cls, region_point=None, opt_pose=True, perms=None, trace=None,
+                pool_override=None):
         bs = x.size(0)
         xm, nm = self.backbone(x)
         xm = self.xyz_final(self.XYZNet(xm))
@@ -456,7 +467,7 @@ class KRRNOracle(nn.Module):
             return out
         xe = torch.gather(xyz.reshape(bs, 3, -1), -1, choose.repeat(1, 3, 1)).permute(0, 2, 1)
         ne = torch.gather(nml.reshape(bs, 3, -1), -1, choose.repeat(1, 3, 1)).permute(0, 2, 1)
-        feat = self.fusion(p_emb, xe, ne, perms=perms, trace=trace)
+        feat = self.fusion(p_emb, xe, ne, perms=perms, trace=trace, pool_override=pool_override)
         n = p_emb.size(1)
         one_hot = torch.zeros(bs, C).scatter_(1, cls.view(-1, 1).long(), 1)
         feat = torch.cat([feat, one_hot.unsqueeze(1).repeat(1, n, 1)], 2)

@@ -63,6 +63,23 @@ def pnp_ransac(obj, img, K4, subsets, thr=1.0):
     return R.reshape(3, 3), t, cnt, mask.astype(bool), best.value
 
 
+def pnp_hypotheses(obj, img, K4, subsets, thr=1.0):
+    """Diagnostics: every RANSAC hypothesis -> (R [H,3,3] f32, t [H,3] f32, counts [H])."""
+    obj = np.ascontiguousarray(obj, dtype=np.float32)
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    K4 = np.ascontiguousarray(K4, dtype=np.float32)
+    subsets = np.ascontiguousarray(subsets, dtype=np.int32)
+    H = len(subsets)
+    R = np.zeros((H, 9), np.float32)
+    t = np.zeros((H, 3), np.float32)
+    cnt = np.zeros(H, np.int32)
+    lib = _load()
+    lib.oracle_pnp_hypotheses.restype = None
+    lib.oracle_pnp_hypotheses(_p(obj), _p(img), ctypes.c_int(len(obj)), _p(K4), _p(subsets), ctypes.c_int(H),
+                              ctypes.c_float(thr), _p(R), _p(t), _p(cnt))
+    return R.reshape(H, 3, 3), t, cnt
+
+
 def rotation_from_axis_angle(rvec):
     """Rodrigues (kornia.angle_axis_to_rotation_matrix semantics, float64)."""
     rvec = np.asarray(rvec, dtype=np.float64)

@@ -398,6 +398,36 @@ double oracle_epnp(const double* pw, const double* uv, int n, const double* K4, 
   return epnp(pw, uv, n, cam, R, t);
 }
 
+/* Every hypothesis of oracle_pnp_ransac (diagnostics): f32-cast pose and inlier count. */
+void oracle_pnp_hypotheses(const float* obj, const float* img, int P, const float* K4, const int* subsets, int H,
+                           float thr, float* R_out, float* t_out, int* cnt_out) {
+  Cam cam = {K4[0], K4[1], K4[2], K4[3]};
+  const float thr2 = thr * thr;
+  for (int h = 0; h < H; ++h) {
+    double spw[15], suv[10], R[9], t[3];
+    for (int i = 0; i < 5; ++i) {
+      const int id = subsets[5 * h + i];
+      for (int k = 0; k < 3; ++k) spw[3 * i + k] = obj[3 * id + k];
+      for (int k = 0; k < 2; ++k) suv[2 * i + k] = img[2 * id + k];
+    }
+    epnp(spw, suv, 5, cam, R, t);
+    int cnt = 0;
+    for (int p = 0; p < P; ++p) {
+      const float X = obj[3 * p], Y = obj[3 * p + 1], Z = obj[3 * p + 2];
+      const float xc = (float)R[0] * X + (float)R[1] * Y + (float)R[2] * Z + (float)t[0];
+      const float yc = (float)R[3] * X + (float)R[4] * Y + (float)R[5] * Z + (float)t[1];
+      const float zc = (float)R[6] * X + (float)R[7] * Y + (float)R[8] * Z + (float)t[2];
+      const float iz = 1.0f / zc;
+      const float du = img[2 * p] - ((float)cam.fu * xc * iz + (float)cam.uc);
+      const float dv = img[2 * p + 1] - ((float)cam.fv * yc * iz + (float)cam.vc);
+      if (du * du + dv * dv <= thr2) ++cnt;
+    }
+    for (int i = 0; i < 9; ++i) R_out[9 * h + i] = (float)R[i];
+    for (int i = 0; i < 3; ++i) t_out[3 * h + i] = (float)t[i];
+    cnt_out[h] = cnt;
+  }
+}
+
 /*
  * RANSAC with caller-given hypothesis subsets.
  * obj: P x 3 (f32, metres, model frame), img: P x 2 (f32, pixels), K4 = fx, fy, cx, cy.

@@ -29,7 +29,7 @@ _F = ctypes.c_float
 _U64 = ctypes.c_uint64
 SIGNATURES = {
     "krrn_conv2d_f32": [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I, _P, _P, _P, _I,
-                        _P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+                        _P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P],
 }
 
 

@@ -61,6 +61,11 @@ struct ConvArgs {
   int Ho, Wo, osy, osx, ooy, oox;
   int relu;
   int M;
+  // split-K: blockIdx.y = z owns k-tiles [z*kt_per, (z+1)*kt_per) and writes its raw partial
+  // sums to ws[z][M][N]; krrn_splitk_epilogue then adds the partials in z order and applies
+  // the epilogue (deterministic: no atomics).
+  int kt_per;
+  float* ws;
 };
 
 template <int BM, int BN, int BK, int WGM>
@@ -121,9 +126,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
     a_ix[i] = gx * a.in_s;
     a_base[i] = a.in + (size_t)b * a.Hi * a.Wi * a.in_cs + a.in_co;
   }
-  int tap = kq / a.cin;
-  int cc = kq - tap * a.cin;
-  int kk = kq;  // absolute k of this thread's staged float4s
+  const int nkt_all = (a.K + BK - 1) / BK;
+  const int kt0 = a.ws ? blockIdx.y * a.kt_per : 0;
+  const int nkt = a.ws ? min(a.kt_per, nkt_all - kt0) : nkt_all;
+  int kk = kt0 * BK + kq;  // absolute k of this thread's staged float4s
+  int tap = kk / a.cin;
+  int cc = kk - tap * a.cin;
 
   auto load_tile = [&](Stage<AL, BL>& st) {
     int ddy = 0, ddx = 0;
@@ -201,7 +209,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
   };
 
   // ---- main loop: loads two tiles ahead, LDS double-buffered, unrolled by 2 ---------------
-  const int nkt = (a.K + BK - 1) / BK;
   Stage<AL, BL> s0, s1;
   load_tile(s0);
   if (nkt > 1) load_tile(s1);
@@ -220,6 +227,24 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
   }
 
   // ---- epilogue -----------------------------------------------------------------------
+  if constexpr (!NCHW) {
+    if (a.ws) {  // split-K partial: raw sums, N-contiguous rows
+      float* w = a.ws + (size_t)blockIdx.y * a.M * a.N;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int n = n0 + wn * C::WTN + j * 32 + frow;
+          if (n >= a.N) continue;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * C::WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            if (m < a.M) w[(size_t)m * a.N + n] = acc[i][j][r];
+          }
+        }
+      return;
+    }
+  }
   const int HWo = a.Ho * a.Wo;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -265,10 +290,44 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
     }
 }
 
+// Sum of the split-K partials in z order + the conv epilogue (NHWC output). One thread per
+// (m, 4 channels).
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a, int splits) {
+  const int nq = a.n_store >> 2;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)a.M * nq) return;
+  const int m = (int)(t / nq);
+  const int n = (int)(t - (long long)m * nq) * 4;
+  const size_t plane = (size_t)a.M * a.N;
+  const float* w = a.ws + (size_t)m * a.N + n;
+  f32x4 v = *reinterpret_cast<const f32x4*>(w);
+  for (int z = 1; z < splits; ++z) v += *reinterpret_cast<const f32x4*>(w + z * plane);
+  const int HWg = a.Hg * a.Wg;
+  const int b = m / HWg;
+  const int rr = m - b * HWg;
+  const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
+  const int oy = gy * a.osy + a.ooy, ox = gx * a.osx + a.oox;
+  const size_t pix = ((size_t)b * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float x = v[q] * (a.scale ? a.scale[n + q] : 1.f) + (a.bias ? a.bias[n + q] : 0.f);
+    if (a.bias2) x += a.bias2[(size_t)(m / a.b2_div) * a.N + n + q];
+    if (a.res) x += a.res[pix * a.res_cs + a.res_co + n + q];
+    if (a.relu) x = fmaxf(x, 0.f);
+    a.out[pix * a.out_cs + a.out_co + n + q] = x;
+  }
+}
+
 template <int BM, int BN, int BK, int WGM, bool NCHW>
-int launch(const ConvArgs& a, hipStream_t s) {
+int launch(const ConvArgs& a, int splits, hipStream_t s) {
   const int nwg = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
-  hipLaunchKernelGGL((conv_gemm_f32_kernel<BM, BN, BK, WGM, NCHW>), dim3(nwg), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_f32_kernel<BM, BN, BK, WGM, NCHW>), dim3(nwg, a.ws ? splits : 1), dim3(256), 0, s,
+                     a);
+  if (a.ws) {
+    const long long threads = (long long)a.M * (a.n_store >> 2);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a,
+                       splits);
+  }
   return krrn_launch_status();
 }
 
@@ -281,7 +340,8 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
                              const float* wt, int N, int n_store, const float* scale, const float* bias,
                              const float* bias2, int b2_div, const float* res, int res_cs, int res_co,
                              float* out, int out_cs, int out_co, int Ho, int Wo, int osy, int osx, int ooy,
-                             int oox, int relu, int out_nchw, int tile, void* stream) {
+                             int oox, int relu, int out_nchw, int tile, int splits, float* workspace,
+                             void* stream) {
   if (!in || !wt || !out || !tap_dy || !tap_dx) return KRRN_EARG;
   if (ntaps < 1 || ntaps > 9 || B < 1 || Hi < 1 || Wi < 1 || Hg < 1 || Wg < 1 || N < 1) return KRRN_ESHAPE;
   if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
@@ -292,6 +352,12 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
   if (tile < 0 || tile > 8) return KRRN_EARG;
   const long long M = (long long)B * Hg * Wg;
   if (M > 0x7fffffffLL) return KRRN_ESHAPE;
+  if (splits < 1 || splits > 64) return KRRN_EARG;
+  if (splits > 1) {
+    if (!workspace || out_nchw) return KRRN_EARG;
+    if ((N & 3) || (n_store & 3)) return KRRN_EALIGN;
+    if (!krrn_aligned16(workspace)) return KRRN_EALIGN;
+  }
   ConvArgs a;
   a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.Hi = Hi; a.Wi = Wi; a.cin = cin;
   a.Hg = Hg; a.Wg = Wg; a.in_s = in_s; a.ntaps = ntaps;
@@ -302,25 +368,37 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
   a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.Ho = Ho; a.Wo = Wo;
   a.osy = osy; a.osx = osx; a.ooy = ooy; a.oox = oox; a.relu = relu; a.M = (int)M;
   hipStream_t s = (hipStream_t)stream;
-  if (tile == 0) {
+  if (tile == 0) {  // same rule as runtime.conv_tile
     const long long wg128 = (long long)krrn_cdiv(a.M, 128) * krrn_cdiv(N, 128);
-    if (N <= 32) tile = 5;
-    else if (N <= 64) tile = (krrn_cdiv(a.M, 128) >= 512) ? 2 : 3;
-    else tile = (wg128 >= 512) ? 1 : 3;
+    if (out_nchw) tile = wg128 >= 512 ? 1 : 3;
+    else if (N <= 32) tile = 6;
+    else if (N >= 128 && a.K >= 512 && wg128 >= 2048) tile = 4;
+    else tile = 8;
+  }
+  a.ws = nullptr;
+  a.kt_per = 0;
+  if (splits > 1) {
+    // every split gets kt_per k-tiles of the chosen tile's BK; the host sized `splits` so
+    // that none is empty (splits <= cdiv(K, BK))
+    const int bk = (tile == 1 || tile == 2 || tile == 3 || tile == 5) ? 16 : 32;
+    const int nkt = krrn_cdiv(a.K, bk);
+    a.kt_per = krrn_cdiv(nkt, splits);
+    splits = krrn_cdiv(nkt, a.kt_per);
+    if (splits > 1) a.ws = workspace;
   }
   if (out_nchw) {
-    if (tile == 1 || tile == 4) return launch<128, 128, 16, 2, true>(a, s);
-    if (tile == 2 || tile == 7) return launch<128, 64, 16, 2, true>(a, s);
-    return launch<64, 64, 16, 2, true>(a, s);
+    if (tile == 1 || tile == 4) return launch<128, 128, 16, 2, true>(a, 1, s);
+    if (tile == 2 || tile == 7) return launch<128, 64, 16, 2, true>(a, 1, s);
+    return launch<64, 64, 16, 2, true>(a, 1, s);
   }
   switch (tile) {
-    case 1: return launch<128, 128, 16, 2, false>(a, s);
-    case 2: return launch<128, 64, 16, 2, false>(a, s);
-    case 3: return launch<64, 64, 16, 2, false>(a, s);
-    case 4: return launch<128, 128, 32, 2, false>(a, s);
-    case 5: return launch<256, 32, 16, 4, false>(a, s);
-    case 6: return launch<128, 32, 32, 4, false>(a, s);
-    case 7: return launch<128, 64, 32, 2, false>(a, s);
-    default: return launch<64, 64, 32, 2, false>(a, s);
+    case 1: return launch<128, 128, 16, 2, false>(a, splits, s);
+    case 2: return launch<128, 64, 16, 2, false>(a, splits, s);
+    case 3: return launch<64, 64, 16, 2, false>(a, splits, s);
+    case 4: return launch<128, 128, 32, 2, false>(a, splits, s);
+    case 5: return launch<256, 32, 16, 4, false>(a, splits, s);
+    case 6: return launch<128, 32, 32, 4, false>(a, splits, s);
+    case 7: return launch<128, 64, 32, 2, false>(a, splits, s);
+    default: return launch<64, 64, 32, 2, false>(a, splits, s);
   }
 }

@@ -19,6 +19,7 @@
 namespace {
 
 constexpr int kKnnThreads = 256;
+constexpr int kKnnParts = 4;     // lanes per query, each scanning every 4th candidate
 constexpr int kKnnChunk = 1024;  // candidates per LDS stage
 constexpr int kKnnKmax = 16;
 
@@ -45,34 +46,44 @@ __device__ __forceinline__ float knn_inner(const float* a, const float* b) {
   return s;
 }
 
-template <int D>
+// (d, index) lexicographic order: the stable-sort order the oracle pins (ties -> lower index).
+__device__ __forceinline__ bool knn_less(float d0, int i0, float d1, int i1) {
+  return d0 < d1 || (d0 == d1 && i0 < i1);
+}
+
+// One query = kKnnParts adjacent lanes. Lane `part` keeps the ascending top-KS of candidates
+// j = part (mod kKnnParts) in registers (KS = k + drop rounded up to an instantiated size);
+// the partial lists are then merged in (d, index) order, which equals the global stable
+// top-KS because (d, index) is a total order. Block = 64 queries.
+template <int D, int KS>
 __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
     const float* __restrict__ q, long long q_bs, int q_st, int nq, const int* __restrict__ qidx,
     const float* __restrict__ c, long long c_bs, int c_st, int nc, int K, int drop, int mode,
     int* __restrict__ out) {
 #pragma clang fp contract(off)
   constexpr int DP = D == 3 ? 4 : 12;  // LDS record: coords + |c|^2 (+ pad)
-  __shared__ __attribute__((aligned(16))) float sc[kKnnChunk * DP];
+  constexpr int QPB = kKnnThreads / kKnnParts;
+  constexpr int STAGE = kKnnChunk * DP;
+  constexpr int MERGE = kKnnThreads * KS * 2;
+  __shared__ __attribute__((aligned(16))) float sc[STAGE > MERGE ? STAGE : MERGE];
   const int b = blockIdx.y;
-  const int t = blockIdx.x * kKnnThreads + threadIdx.x;
+  const int part = threadIdx.x % kKnnParts;
+  const int ql = threadIdx.x / kKnnParts;
+  const int t = blockIdx.x * QPB + ql;
   const bool active = t < nq;
   float qp[D];
   float qn = 0.f;
-  if (active) {
-    const int qi = qidx ? qidx[t] : t;
+  {
+    const int qi = active ? (qidx ? qidx[t] : t) : 0;
     const float* src = q + b * q_bs + (long long)qi * q_st;
 #pragma unroll
     for (int i = 0; i < D; ++i) qp[i] = src[i];
     qn = knn_sqnorm<D>(qp);
-  } else {
-#pragma unroll
-    for (int i = 0; i < D; ++i) qp[i] = 0.f;
   }
-  float bd[kKnnKmax];
-  int bi[kKnnKmax];
+  float bd[KS];
+  int bi[KS];
 #pragma unroll
-  for (int i = 0; i < kKnnKmax; ++i) { bd[i] = INFINITY; bi[i] = 0x7fffffff; }
-  float thr = INFINITY;
+  for (int i = 0; i < KS; ++i) { bd[i] = INFINITY; bi[i] = 0x7fffffff; }
 
   const float* cb = c + b * c_bs;
   for (int j0 = 0; j0 < nc; j0 += kKnnChunk) {
@@ -89,46 +100,79 @@ __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
       dst[D] = knn_sqnorm<D>(p);
     }
     __syncthreads();
-    if (active) {
-      for (int j = 0; j < cnt; ++j) {
-        const float* p = sc + j * DP;
-        const float inner = knn_inner<D>(qp, p);
-        const float cn = p[D];
-        const float d = mode == 0 ? ((inner * -2.f) + cn) + qn : (cn + qn) - 2.f * inner;
-        if (d < thr) {
-          // branch-free insertion into the ascending list: the new entry goes in front of the
-          // first strictly larger one (so equal distances keep the earlier = lower index
-          // first) and every later slot takes its predecessor. Slots >= K are scratch.
-          const int ni = j0 + j;
-          bool ins = false;
-          float cd = 0.f;
-          int ci = 0;
+    for (int j = part; j < cnt; j += kKnnParts) {
+      const float* p = sc + j * DP;
+      const float inner = knn_inner<D>(qp, p);
+      const float cn = p[D];
+      const float d = mode == 0 ? ((inner * -2.f) + cn) + qn : (cn + qn) - 2.f * inner;
+      if (d < bd[KS - 1]) {
+        // insertion in front of the first strictly larger entry (candidates of one lane arrive
+        // in increasing index, so equal distances stay in index order); branch-free shift
+        const int ni = j0 + j;
+        bool ins = false;
+        float cd = 0.f;
+        int ci = 0;
 #pragma unroll
-          for (int s = 0; s < kKnnKmax; ++s) {
-            const bool here = !ins && (d < bd[s]);
-            const float od = bd[s];
-            const int oi = bi[s];
-            bd[s] = ins ? cd : (here ? d : od);
-            bi[s] = ins ? ci : (here ? ni : oi);
-            cd = od;
-            ci = oi;
-            ins = ins || here;
-          }
-          float tv = INFINITY;
-#pragma unroll
-          for (int s = 0; s < kKnnKmax; ++s) tv = (s == K - 1) ? bd[s] : tv;
-          thr = tv;
+        for (int s2 = 0; s2 < KS; ++s2) {
+          const bool here = !ins && (d < bd[s2]);
+          const float od = bd[s2];
+          const int oi = bi[s2];
+          bd[s2] = ins ? cd : (here ? d : od);
+          bi[s2] = ins ? ci : (here ? ni : oi);
+          cd = od;
+          ci = oi;
+          ins = ins || here;
         }
       }
     }
   }
-  if (active) {
-    const int ko = K - drop;
-    int* o = out + ((long long)b * nq + t) * ko;
+  // ---- merge the kKnnParts partial lists of each query -------------------------------------
+  __syncthreads();
+  float* md = sc;
+  int* mi = reinterpret_cast<int*>(sc + kKnnThreads * KS);
 #pragma unroll
-    for (int s = 0; s < kKnnKmax; ++s)
-      if (s >= drop && s < K) o[s - drop] = bi[s];
+  for (int s2 = 0; s2 < KS; ++s2) {
+    md[threadIdx.x * KS + s2] = bd[s2];
+    mi[threadIdx.x * KS + s2] = bi[s2];
   }
+  __syncthreads();
+  if (!active || part != 0) return;
+  const int base = threadIdx.x * KS;  // lists of lanes threadIdx.x .. threadIdx.x + 3
+  int hp[kKnnParts];
+#pragma unroll
+  for (int r = 0; r < kKnnParts; ++r) hp[r] = 0;
+  const int ko = K - drop;
+  int* o = out + ((long long)b * nq + t) * ko;
+  for (int s2 = 0; s2 < K; ++s2) {
+    float best_d = INFINITY;
+    int best_i = 0x7fffffff, best_r = 0;
+#pragma unroll
+    for (int r = 0; r < kKnnParts; ++r) {
+      if (hp[r] < KS) {
+        const float dd = md[base + r * KS + hp[r]];
+        const int ii = mi[base + r * KS + hp[r]];
+        if (knn_less(dd, ii, best_d, best_i)) { best_d = dd; best_i = ii; best_r = r; }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kKnnParts; ++r) hp[r] += (r == best_r);
+    if (s2 >= drop) o[s2 - drop] = best_i;
+  }
+}
+
+template <int D>
+void knn_launch(dim3 grid, hipStream_t s, const float* q, long long q_bs, int q_st, int nq, const int* qidx,
+                const float* c, long long c_bs, int c_st, int nc, int K, int drop, int mode, int* out) {
+#define KNN_CASE(KS)                                                                                   \
+  hipLaunchKernelGGL((knn_kernel<D, KS>), grid, dim3(kKnnThreads), 0, s, q, q_bs, q_st, nq, qidx, c, c_bs, \
+                     c_st, nc, K, drop, mode, out)
+  if (K <= 1) KNN_CASE(1);
+  else if (K <= 2) KNN_CASE(2);
+  else if (K <= 5) KNN_CASE(5);
+  else if (K <= 8) KNN_CASE(8);
+  else if (K <= 11) KNN_CASE(11);
+  else KNN_CASE(16);
+#undef KNN_CASE
 }
 
 }  // namespace
@@ -142,14 +186,12 @@ KRRN_API int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, cons
   if (k + (drop_first ? 1 : 0) > nc) return KRRN_ESHAPE;
   if (mode != 0 && mode != 1) return KRRN_EARG;
   const int K = k + (drop_first ? 1 : 0);
-  dim3 grid(krrn_cdiv(nq, kKnnThreads), B);
+  dim3 grid(krrn_cdiv(nq, kKnnThreads / kKnnParts), B);
   hipStream_t s = (hipStream_t)stream;
   if (d == 3)
-    hipLaunchKernelGGL(knn_kernel<3>, grid, dim3(kKnnThreads), 0, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc,
-                       K, drop_first ? 1 : 0, mode, out);
+    knn_launch<3>(grid, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, drop_first ? 1 : 0, mode, out);
   else
-    hipLaunchKernelGGL(knn_kernel<9>, grid, dim3(kKnnThreads), 0, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc,
-                       K, drop_first ? 1 : 0, mode, out);
+    knn_launch<9>(grid, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, drop_first ? 1 : 0, mode, out);
   return krrn_launch_status();
 }
 
@@ -158,11 +200,18 @@ KRRN_API int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, cons
 // ------------------------------------------------------------------------------------------
 namespace {
 
-constexpr int kGcnThreads = 128;
-constexpr int kGcnPts = 8;  // points per block
+constexpr int kGcnThreads = 256;
+constexpr int kGcnPts = 8;  // points per block: 32 lanes x 4 channels each per point
 constexpr int kGcnKmax = 16;
 
-template <int D, bool HAS_Y>
+// Block = 8 points of one crop; a point is 32 lanes, lane l owning channels 4l.. (+128 per
+// step for C = 512). For each support s and neighbour j a lane reads one float4 of the
+// neighbour's Y row (512-B coalesced per point), so every neighbour row segment
+// Y[nj, C + s*C : C + (s+1)*C] is one wide read. The block -> (crop, points) map is XCD-aware:
+// consecutive point groups of one crop share an XCD and its L2, where their overlapping
+// neighbourhoods (choose is pixel-ordered, so neighbours have nearby indices) hit.
+// KC = compile-time k (0: runtime k).
+template <int D, bool HAS_Y, int KC>
 __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
     const int* __restrict__ idx, int n, int k, const float* __restrict__ v, long long v_bs, int v_st,
     const float* __restrict__ dn, int S, int C, const float* __restrict__ Y,
@@ -170,15 +219,18 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
     long long o_bs, int o_st) {
   __shared__ float sdir[kGcnPts * kGcnKmax * D];
   __shared__ int snb[kGcnPts * kGcnKmax];
-  const int b = blockIdx.y;
-  const int p0 = blockIdx.x * kGcnPts;
+  const int gx = gridDim.x;
+  const int lin = krrn_xcd_remap(blockIdx.x + gx * blockIdx.y, gx * gridDim.y);
+  const int b = lin / gx;
+  const int p0 = (lin - b * gx) * kGcnPts;
   const int np = min(kGcnPts, n - p0);
+  const int kk = KC ? KC : k;
   const float* vb = v + b * v_bs;
   // 1) neighbour directions, F.normalize(v[j] - v[i], dim=-1) (gcn3d.py:60-69)
-  for (int e = threadIdx.x; e < np * k; e += kGcnThreads) {
-    const int p = e / k, j = e - (e / k) * k;
+  for (int e = threadIdx.x; e < np * kk; e += kGcnThreads) {
+    const int p = e / kk, j = e - (e / kk) * kk;
     const int pi = p0 + p;
-    const int nj = idx[((long long)b * n + pi) * k + j];
+    const int nj = idx[((long long)b * n + pi) * kk + j];
     snb[p * kGcnKmax + j] = nj;
     float dv[D];
     float ss = 0.f;
@@ -192,45 +244,45 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
     for (int i = 0; i < D; ++i) sdir[(p * kGcnKmax + j) * D + i] = dv[i] / nr;
   }
   __syncthreads();
+  const int p = threadIdx.x >> 5, l = threadIdx.x & 31;
+  if (p >= np) return;
+  const int pi = p0 + p;
   const int SC = S * C;
   const long long yrow = (long long)(S + 1) * C;
   const float* yb = HAS_Y ? Y + b * (long long)n * yrow : nullptr;
-  for (int c = threadIdx.x; c < C; c += kGcnThreads) {
-    float acc[kGcnPts];
-#pragma unroll
-    for (int p = 0; p < kGcnPts; ++p) acc[p] = 0.f;
+  const float* dp = sdir + p * kGcnKmax * D;
+  const int* nbp = snb + p * kGcnKmax;
+  for (int c = 4 * l; c < C; c += 128) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < S; ++s) {
-      float w[D];
+      f32x4 w[D];
 #pragma unroll
-      for (int i = 0; i < D; ++i) w[i] = dn[(long long)i * SC + s * C + c];
+      for (int i = 0; i < D; ++i) w[i] = *reinterpret_cast<const f32x4*>(dn + (long long)i * SC + s * C + c);
+      f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-      for (int p = 0; p < kGcnPts; ++p) {
-        if (p < np) {
-          float m = -INFINITY;
-          for (int j = 0; j < k; ++j) {
-            const float* dr = sdir + (p * kGcnKmax + j) * D;
-            float th = 0.f;
+      for (int j = 0; j < (KC ? KC : kGcnKmax); ++j) {
+        if (!KC && j >= kk) break;
+        const float* dr = dp + j * D;
+        f32x4 th = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < D; ++i) th += dr[i] * w[i];
-            th = fmaxf(th, 0.f);
-            float val = th;
-            if constexpr (HAS_Y) val = th * yb[(long long)snb[p * kGcnKmax + j] * yrow + C + s * C + c];
-            m = fmaxf(m, val);
-          }
-          acc[p] += m;
-        }
+        for (int i = 0; i < D; ++i) th += dr[i] * w[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) th[q] = fmaxf(th[q], 0.f);
+        f32x4 val = th;
+        if constexpr (HAS_Y) val = th * *reinterpret_cast<const f32x4*>(yb + (long long)nbp[j] * yrow + C + s * C + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], val[q]);
       }
+      acc += m;
     }
+    f32x4 o = acc;
+    if constexpr (HAS_Y) o = *reinterpret_cast<const f32x4*>(yb + (long long)pi * yrow + c) + o;
 #pragma unroll
-    for (int p = 0; p < kGcnPts; ++p) {
-      if (p < np) {
-        float o = acc[p];
-        if constexpr (HAS_Y) o = yb[(long long)(p0 + p) * yrow + c] + o;
-        if (bn_s) o = o * bn_s[c] + bn_b[c];
-        if (relu) o = fmaxf(o, 0.f);
-        out[b * o_bs + (long long)(p0 + p) * o_st + c] = o;
-      }
+    for (int q = 0; q < 4; ++q) {
+      if (bn_s) o[q] = o[q] * bn_s[c + q] + bn_b[c + q];
+      if (relu) o[q] = fmaxf(o[q], 0.f);
     }
+    *reinterpret_cast<f32x4*>(out + b * o_bs + (long long)pi * o_st + c) = o;
   }
 }
 
@@ -244,16 +296,23 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   if ((bn_scale == nullptr) != (bn_bias == nullptr)) return KRRN_EARG;
   if (d != 3 && d != 9) return KRRN_ESHAPE;
   if (k < 1 || k > kGcnKmax || n < 1 || S < 1 || C < 1 || B < 1) return KRRN_ESHAPE;
+  if ((C & 3) || (o_st & 3) || (o_bs & 3) || !krrn_aligned16(out) || !krrn_aligned16(dn)) return KRRN_EALIGN;
+  if (Y && !krrn_aligned16(Y)) return KRRN_EALIGN;
   dim3 grid(krrn_cdiv(n, kGcnPts), B);
   hipStream_t s = (hipStream_t)stream;
-#define KRRN_GCN_LAUNCH(DD, HY)                                                                         \
-  hipLaunchKernelGGL((gcn_conv_kernel<DD, HY>), grid, dim3(kGcnThreads), 0, s, idx, n, k, v, v_bs, v_st, dn, \
-                     S, C, Y, bn_scale, bn_bias, relu, out, o_bs, o_st)
+#define KRRN_GCN_LAUNCH(DD, HY, KC)                                                                         \
+  hipLaunchKernelGGL((gcn_conv_kernel<DD, HY, KC>), grid, dim3(kGcnThreads), 0, s, idx, n, k, v, v_bs, v_st, \
+                     dn, S, C, Y, bn_scale, bn_bias, relu, out, o_bs, o_st)
+#define KRRN_GCN_K(DD, HY)                 \
+  if (k == 10) KRRN_GCN_LAUNCH(DD, HY, 10); \
+  else if (k == 7) KRRN_GCN_LAUNCH(DD, HY, 7); \
+  else KRRN_GCN_LAUNCH(DD, HY, 0)
   if (d == 3) {
-    if (Y) KRRN_GCN_LAUNCH(3, true); else KRRN_GCN_LAUNCH(3, false);
+    if (Y) { KRRN_GCN_K(3, true); } else { KRRN_GCN_K(3, false); }
   } else {
-    if (Y) KRRN_GCN_LAUNCH(9, true); else KRRN_GCN_LAUNCH(9, false);
+    if (Y) { KRRN_GCN_K(9, true); } else { KRRN_GCN_K(9, false); }
   }
+#undef KRRN_GCN_K
 #undef KRRN_GCN_LAUNCH
   return krrn_launch_status();
 }

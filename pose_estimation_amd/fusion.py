@@ -122,14 +122,15 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     i32 = torch.int32
     idx0 = plan.buf((B, N, k0), i32)
     F0 = plan.buf((B, N, 384))
-    Y1 = plan.buf((B * N, (S + 1) * 128))
+    # one GEMM-output buffer per branch: the three branches run on their own plan streams
+    Y1 = [plan.buf((B * N, (S + 1) * 128)) for _ in range(3)]
     feat1 = plan.buf((B, N, 384))
-    nb4 = plan.buf((B, N1, 4), i32)
+    nb4 = {br: plan.buf((B, N1, 4), i32) for br in ("v", "x", "n")}
     V1 = plan.buf((B, N1, 9))
     FP1 = plan.buf((B, N1, 384))
     PV1 = plan.buf((B, N1, 9))
     idx1 = plan.buf((B, N1, k1), i32)
-    Y2 = plan.buf((B * N1, (S + 1) * 128))
+    Y2 = [plan.buf((B * N1, (S + 1) * 128)) for _ in range(3)]
     feat2 = plan.buf((B, N1, 384))
     nb4b = plan.buf((B, N2, 4), i32)
     FP2 = plan.buf((B, N2, 384))
@@ -167,47 +168,57 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
         return ptr(t) if floats == 0 else type(ptr(t))(t.data_ptr() + 4 * floats)
 
     # level 0: idx0 = kNN(cloud, 10) (fusion.py:175)
+    # level 0: idx0 = kNN(cloud, 10) (fusion.py:175); then the v / x / n branches (conv_0,
+    # conv_1 + BN + ReLU, pool_1_*) are independent until the concat: branch bi on stream bi
     knn(off(p9, 0), N * 9, 9, N, ptr(None), off(p9, 0), N * 9, 9, N, 3, k0, 1, 0, idx0)
+    plan.fork([1, 2])
     for bi, br in enumerate(("v", "x", "n")):
-        c0 = getattr(fu, f"conv_0_{br}")
-        gcn(idx0, N, k0, off(p9, 3 * bi), N * 9, 3, _dn(c0.directions, dev), 128, None, None, True,
-            off(F0, 128 * bi), N * 384, 384)
-    for bi, br in enumerate(("v", "x", "n")):
-        c1 = getattr(fu, f"conv_1_{br}")
-        gemm(F0, 384, 128 * bi, B * N, c1, Y1)
-        gcn(idx0, N, k0, off(p9, 3 * bi), N * 9, 3, _dn(c1.directions, dev), 128, Y1,
-            _bn1d(getattr(fu, f"bn1_{br}"), dev), True, off(feat1, 128 * bi), N * 384, 384)
-    # pools (fusion.py:197-202): per-branch kNN(4) at the sampled rows, max, vertex gather
-    for bi, br in enumerate(("v", "x", "n")):
-        perm = perms[br]
-        knn(off(p9, 3 * bi), N * 9, 9, N1, ptr(perm), off(p9, 3 * bi), N * 9, 9, N, 3, 4, 1, 0, nb4)
-        plan.add("krrn_pool_max_f32", ptr(nb4), N1, 4, off(feat1, 128 * bi), N * 384, 384, 128,
-                 off(FP1, 128 * bi), N1 * 384, 384, B)
-        plan.add("krrn_gather_rows_f32", ptr(perm), 0, 0, N1, off(p9, 3 * bi), N * 9, 9, off(V1, 3 * bi), N1 * 9, 9,
-                 3, B)
+        with plan.on_stream(bi):
+            c0 = getattr(fu, f"conv_0_{br}")
+            gcn(idx0, N, k0, off(p9, 3 * bi), N * 9, 3, _dn(c0.directions, dev), 128, None, None, True,
+                off(F0, 128 * bi), N * 384, 384)
+            c1 = getattr(fu, f"conv_1_{br}")
+            gemm(F0, 384, 128 * bi, B * N, c1, Y1[bi])
+            gcn(idx0, N, k0, off(p9, 3 * bi), N * 9, 3, _dn(c1.directions, dev), 128, Y1[bi],
+                _bn1d(getattr(fu, f"bn1_{br}"), dev), True, off(feat1, 128 * bi), N * 384, 384)
+            # pools (fusion.py:197-202): kNN(4) at the sampled rows, max, vertex gather
+            perm = perms[br]
+            knn(off(p9, 3 * bi), N * 9, 9, N1, ptr(perm), off(p9, 3 * bi), N * 9, 9, N, 3, 4, 1, 0, nb4[br])
+            plan.add("krrn_pool_max_f32", ptr(nb4[br]), N1, 4, off(feat1, 128 * bi), N * 384, 384, 128,
+                     off(FP1, 128 * bi), N1 * 384, 384, B)
+            plan.add("krrn_gather_rows_f32", ptr(perm), 0, 0, N1, off(p9, 3 * bi), N * 9, 9, off(V1, 3 * bi),
+                     N1 * 9, 9, 3, B)
     plan.add("krrn_gather_rows_f32", ptr(perms["p1"]), 0, 0, N1, off(p9, 0), N * 9, 9, off(PV1, 0), N1 * 9, 9, 9, B)
+    plan.join([1, 2])
     # level 1 (fusion.py:205-216)
     knn(off(V1, 0), N1 * 9, 9, N1, ptr(None), off(V1, 0), N1 * 9, 9, N1, 3, k1, 1, 0, idx1)
+    plan.fork([1, 2, 3])
+    with plan.on_stream(3):  # nearest-index to pool_1 (fusion.py:231) only needs PV1
+        knn(off(p9, 0), N * 9, 9, N, ptr(None), off(PV1, 0), N1 * 9, 9, N1, 3, 1, 0, 1, nn1)
     for bi, br in enumerate(("v", "x", "n")):
-        c2 = getattr(fu, f"conv_2_{br}")
-        gemm(FP1, 384, 128 * bi, B * N1, c2, Y2)
-        gcn(idx1, N1, k1, off(V1, 3 * bi), N1 * 9, 3, _dn(c2.directions, dev), 128, Y2,
-            _bn1d(getattr(fu, f"bn2_{br}"), dev), True, off(feat2, 128 * bi), N1 * 384, 384)
+        with plan.on_stream(bi):
+            c2 = getattr(fu, f"conv_2_{br}")
+            gemm(FP1, 384, 128 * bi, B * N1, c2, Y2[bi])
+            gcn(idx1, N1, k1, off(V1, 3 * bi), N1 * 9, 3, _dn(c2.directions, dev), 128, Y2[bi],
+                _bn1d(getattr(fu, f"bn2_{br}"), dev), True, off(feat2, 128 * bi), N1 * 384, 384)
+    plan.join([1, 2])
     # pool_2 (fusion.py:219): kNN on pool_1[..., :3] at the sampled rows
     knn(off(PV1, 0), N1 * 9, 9, N2, ptr(perms["p2"]), off(PV1, 0), N1 * 9, 9, N1, 3, 4, 1, 0, nb4b)
     plan.add("krrn_pool_max_f32", ptr(nb4b), N2, 4, off(feat2, 0), N1 * 384, 384, 384, off(FP2, 0), N2 * 384, 384, B)
     plan.add("krrn_gather_rows_f32", ptr(perms["p2"]), 0, 0, N2, off(PV1, 0), N1 * 9, 9, off(PV2, 0), N2 * 9, 9, 9, B)
     # level 2 (fusion.py:223-229): 9-D kNN, Conv_fuse_layer x2, no activation
     knn(off(PV2, 0), N2 * 9, 9, N2, ptr(None), off(PV2, 0), N2 * 9, 9, N2, 9, k2, 1, 0, idx2)
+    plan.fork([3])
+    with plan.on_stream(3):  # nearest-index to pool_2 (fusion.py:232)
+        knn(off(p9, 0), N * 9, 9, N, ptr(None), off(PV2, 0), N2 * 9, 9, N2, 3, 1, 0, 1, nn2)
     gemm(FP2, 384, 0, B * N2, fu.conv_4, Y4)
     gcn(idx2, N2, k2, off(PV2, 0), N2 * 9, 9, _dn(fu.conv_4.directions, dev), 512, Y4, None, False,
         off(fm4, 0), N2 * 512, 512)
     gemm(fm4, 512, 0, B * N2, fu.conv_5, Y5)
     gcn(idx2, N2, k2, off(PV2, 0), N2 * 9, 9, _dn(fu.conv_5.directions, dev), 512, Y5, None, False,
         off(fm5, 0), N2 * 512, 512)
-    # nearest indices (fusion.py:231-232) and the 1280-wide concat (:234-238)
-    knn(off(p9, 0), N * 9, 9, N, ptr(None), off(PV1, 0), N1 * 9, 9, N1, 3, 1, 0, 1, nn1)
-    knn(off(p9, 0), N * 9, 9, N, ptr(None), off(PV2, 0), N2 * 9, 9, N2, 3, 1, 0, 1, nn2)
+    # the 1280-wide concat (fusion.py:234-238)
+    plan.join([3])
     plan.add("krrn_gather_rows_f32", ptr(nn2), 0, N, N, off(fm5, 0), N2 * 512, 512, off(feat, 0), N * 1280, 1280,
              512, B)
     plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat1, 0), N * 384, 384, off(feat, 512), N * 1280, 1280,
@@ -215,5 +226,5 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat2, 0), N1 * 384, 384, off(feat, 896), N * 1280, 1280,
              384, B)
     plan.buffers.append(keep)
-    return feat, dict(idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1, nn2=nn2, feat1=feat1, feat2=feat2, fm5=fm5,
+    return feat, dict(pool_v=nb4["v"], pool_x=nb4["x"], pool_n=nb4["n"], pool2=nb4b, idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1, nn2=nn2, feat1=feat1, feat2=feat2, fm5=fm5,
                       F0=F0, V1=V1, PV1=PV1, PV2=PV2, FP1=FP1, FP2=FP2, fm4=fm4)

@@ -94,7 +94,8 @@ def conv_out_hw(spec: ConvSpec, H: int, W: int) -> Tuple[int, int]:
 
 
 def conv2d(x: Act, spec: ConvSpec, out: Act, res: Optional[Act] = None, relu: bool = False,
-           bias2: Optional[torch.Tensor] = None, b2_div: int = 1, tile: int = 0):
+           bias2: Optional[torch.Tensor] = None, b2_div: int = 1, tile: int = 0, splits: int = 1,
+           ws: Optional[torch.Tensor] = None):
     """out = act(BN(conv(x)) [+ bias2] [+ res]) written into ``out``'s channel slice."""
     assert x.cp == spec.cin_p, (x.c, x.cp, spec.cin_p)
     Ho, Wo = out.H, out.W
@@ -113,7 +114,8 @@ def conv2d(x: Act, spec: ConvSpec, out: Act, res: Optional[Act] = None, relu: bo
                   _ptr(bias2), b2_div,
                   _ptr(res.t if res is not None else None), res.cs if res is not None else 0,
                   res.co if res is not None else 0,
-                  _ptr(out.t), out.cs, out.co, Ho, Wo, osy, osx, ooy, oox, int(relu), 0, tile, _stream())
+                  _ptr(out.t), out.cs, out.co, Ho, Wo, osy, osx, ooy, oox, int(relu), 0, tile, splits,
+                  _ptr(ws), _stream())
 
 
 def conv2d_nchw(x: Act, spec: ConvSpec, out: torch.Tensor, n_store: int, relu: bool = False, tile: int = 0):
@@ -126,17 +128,19 @@ def conv2d_nchw(x: Act, spec: ConvSpec, out: torch.Tensor, n_store: int, relu: b
               _ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p,
               Ho, Wo, spec.stride, len(taps), _int_array([t[0] for t in taps]), _int_array([t[1] for t in taps]),
               _ptr(spec.wt[0]), np_, n_store, _ptr(spec.scale), _ptr(spec.bias), _ptr(None), 1,
-              _ptr(None), 0, 0, _ptr(out), C, 0, Ho, Wo, 1, 1, 0, 0, int(relu), 1, tile, _stream())
+              _ptr(None), 0, 0, _ptr(out), C, 0, Ho, Wo, 1, 1, 0, 0, int(relu), 1, tile, 1, _ptr(None), _stream())
 
 
 def gemm(a: torch.Tensor, a_cs: int, a_co: int, M: int, spec: ConvSpec, out: torch.Tensor, out_cs: int,
-         out_co: int, relu: bool = False, bias2: Optional[torch.Tensor] = None, b2_div: int = 1, tile: int = 0):
+         out_co: int, relu: bool = False, bias2: Optional[torch.Tensor] = None, b2_div: int = 1, tile: int = 0,
+         splits: int = 1, ws: Optional[torch.Tensor] = None):
     """Row-major GEMM out[M, :N] = act(scale * (A[M, K] @ W^T) + bias [+ bias2]) via the conv kernel."""
     np_ = pad4(spec.cout)
     _lib.call("krrn_conv2d_f32",
               _ptr(a), a_cs, a_co, 1, 1, M, spec.cin_p, 1, M, 1, 1, _int_array([0]), _int_array([0]),
               _ptr(spec.wt[0]), np_, np_, _ptr(spec.scale), _ptr(spec.bias), _ptr(bias2), b2_div,
-              _ptr(None), 0, 0, _ptr(out), out_cs, out_co, 1, M, 1, 1, 0, 0, int(relu), 0, tile, _stream())
+              _ptr(None), 0, 0, _ptr(out), out_cs, out_co, 1, M, 1, 1, 0, 0, int(relu), 0, tile, splits, _ptr(ws),
+              _stream())
 
 
 # ----------------------------------------------------------------------------------------

@@ -82,7 +82,7 @@ def get_pose(pred, data, num_points: int = NUM_POINTS, n_hyp: int = N_HYP, thr: 
                                        ptr(ext), ptr(lfb), ptr(subsets), n_hyp, float(thr), ptr(ws), ptr(R), ptr(t),
                                        ptr(inl), ptr(mask), B, stream), "krrn_pnp_ransac_f32")
     if return_info:
-        return R, t, {"inliers": inl, "mask": mask, "sel": sel, "subsets": subsets}
+        return R, t, {"inliers": inl, "mask": mask, "sel": sel, "subsets": subsets, "workspace": ws}
     return R, t
 
 

@@ -11,6 +11,7 @@ replayed for the steady-state loop.
 from __future__ import annotations
 
 import ctypes
+import os
 from contextlib import contextmanager
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -115,11 +116,21 @@ class Plan:
         self.cur = 0
         self.nstreams = 1
         self._side: List[torch.cuda.Stream] = []
+        self._scratch: Dict[int, torch.Tensor] = {}
 
     def buf(self, shape, dtype=torch.float32, zero: bool = True) -> torch.Tensor:
         t = (torch.zeros if zero else torch.empty)(tuple(shape), dtype=dtype, device=self.device)
         self.buffers.append(t)
         return t
+
+    def scratch(self, nfloats: int) -> torch.Tensor:
+        """A workspace for the current stream (ops on one stream run in order, so they can share
+        it; a larger request allocates a larger one, earlier ops keep theirs)."""
+        ws = self._scratch.get(self.cur)
+        if ws is None or ws.numel() < nfloats:
+            ws = self.buf((max(nfloats, 1 << 20),), zero=False)
+            self._scratch[self.cur] = ws
+        return ws
 
     def add(self, name: str, *args, meta: Optional[dict] = None):
         self.ops.append(Op(name, list(args) + [Late(_skey(self.cur))], meta, self.cur))
@@ -196,6 +207,23 @@ def conv_tile(M: int, N: int, K: int = 1024, nchw: bool = False) -> int:
     return 8
 
 
+TILE_SHAPES = {1: (128, 128, 16), 2: (128, 64, 16), 3: (64, 64, 16), 4: (128, 128, 32), 5: (256, 32, 16),
+               6: (128, 32, 32), 7: (128, 64, 32), 8: (64, 64, 32)}
+
+
+def conv_splits(M: int, N: int, K: int, tile: int) -> int:
+    """Split-K factor: layers with fewer than 256 output tiles (the 8x8 / 4x4 HRNet branches, M =
+    B*64 / B*16) and a deep K get their k-tiles split across blockIdx.y until ~512 workgroups
+    exist, keeping >= 4 k-tiles per split."""
+    BM, BN, BK = TILE_SHAPES[tile]
+    cd = lambda a, b: (a + b - 1) // b  # noqa: E731
+    tiles = cd(M, BM) * cd(N, BN)
+    nkt = cd(K, BK)
+    if tiles >= 256 or nkt < 8 or N % 4 or os.environ.get("KRRN_SPLITK", "1") == "0":
+        return 1
+    return max(1, min(cd(512, tiles), nkt // 4, 16))
+
+
 CONV_KERNELS = {1: "conv_gemm_f32<128,128,16>", 2: "conv_gemm_f32<128,64,16>", 3: "conv_gemm_f32<64,64,16>",
                 4: "conv_gemm_f32<128,128,32>", 5: "conv_gemm_f32<256,32,16>", 6: "conv_gemm_f32<128,32,32>",
                 7: "conv_gemm_f32<128,64,32>", 8: "conv_gemm_f32<64,64,32>"}
@@ -210,17 +238,21 @@ def _iarr(vals):
 
 def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_store, scale, bias,
              bias2=None, b2_div=1, res=None, res_cs=0, res_co=0, out, out_cs, out_co, Ho, Wo, osy=1, osx=1, ooy=0,
-             oox=0, relu=False, nchw=False, cin=None, cout=None, tag="", tile=None):
+             oox=0, relu=False, nchw=False, cin=None, cout=None, tag="", tile=None, splits=None):
     """Append one krrn_conv2d_f32 launch. Pointers are ctypes values (see `ptr`). cin/cout are the
     logical channel counts used for the algorithmic FLOP count 2*cin*cout*ntaps*M."""
     M = B * Hg * Wg
-    tile = conv_tile(M, N, cin_p * len(taps), nchw) if tile is None else tile
+    K = cin_p * len(taps)
+    tile = conv_tile(M, N, K, nchw) if tile is None else tile
+    if splits is None:
+        splits = 1 if nchw else conv_splits(M, N, K, tile)
+    ws = plan.scratch(splits * M * N) if splits > 1 else None
     cin = cin_p if cin is None else cin
     cout = n_store if cout is None else cout
     flops = 2.0 * cin * cout * len(taps) * M
     plan.add("krrn_conv2d_f32", x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, len(taps), _iarr([t[0] for t in taps]),
              _iarr([t[1] for t in taps]), wt, N, n_store, scale, bias, bias2 if bias2 is not None else P(0), b2_div,
              res if res is not None else P(0), res_cs, res_co, out, out_cs, out_co, Ho, Wo, osy, osx, ooy, oox,
-             int(relu), int(nchw), tile,
-             meta=dict(kernel=CONV_KERNELS[tile] + (",nchw" if nchw else ""), flops=flops, tag=tag, M=M, N=N,
-                       K=cin_p * len(taps)))
+             int(relu), int(nchw), tile, splits, ptr(ws),
+             meta=dict(kernel=CONV_KERNELS[tile] + (",nchw" if nchw else "") + (",splitk" if splits > 1 else ""),
+                       flops=flops, tag=tag, M=M, N=N, K=K, splits=splits))

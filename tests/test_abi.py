@@ -53,7 +53,7 @@ def test_host_side_errors():
     # conv: cin not a multiple of 4 -> KRRN_EALIGN
     taps = (ctypes.c_int * 9)()
     assert lib.krrn_conv2d_f32(fake, 4, 0, 1, 8, 8, 3, 8, 8, 1, 1, taps, taps, fake, 4, 4, N, N, N, 1, N, 0, 0,
-                               fake, 4, 0, 8, 8, 1, 1, 0, 0, 0, 0, 0, N) == -3
+                               fake, 4, 0, 8, 8, 1, 1, 0, 0, 0, 0, 0, 1, N, N) == -3
     # pnp: P < 5 -> KRRN_ESHAPE
     assert lib.krrn_pnp_ransac_f32(fake, 16, fake, 10, fake, 4, fake, fake, fake, fake, fake, fake, 10,
                                    ctypes.c_float(1.0), fake, fake, fake, fake, N, 1, N) == -2

@@ -59,6 +59,37 @@ def test_conv_bn_relu_res(dev, cin, cout, k, s, H, bias, tile):
     assert torch.count_nonzero(out.t[..., cout:]).item() == 0
 
 
+@pytest.mark.parametrize("cin,cout,H,tile,splits", [
+    (144, 144, 4, 8, 10), (72, 72, 8, 8, 4), (36, 36, 15, 8, 3), (18, 20, 30, 6, 16), (144, 144, 4, 3, 64),
+    (64, 128, 9, 7, 5)])
+def test_conv_splitk(dev, cin, cout, H, tile, splits):
+    """Split-K (deterministic slice-ordered reduction + epilogue) vs torch, incl. the in-place
+    residual of the HRNet fuse chain (res aliases out)."""
+    g = torch.Generator().manual_seed(cin + 13 * splits)
+    B = 16
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, H, generator=g)
+    res = torch.randn(B, cout, H, H, generator=g)
+    ref = torch.relu(bn(conv(x)) + res).detach()
+    spec = ops.make_conv(conv, bn, dev)
+    xa = _nhwc(x, dev)
+    out = _nhwc(res, dev)  # accumulate in place: out = relu(conv(x) + out)
+    M, N = B * H * H, ops.pad4(cout)
+    ws = torch.empty(splits * M * N, device=dev)
+    ops.conv2d(xa, spec, out, res=out, relu=True, tile=tile, splits=splits, ws=ws)
+    torch.cuda.synchronize()
+    got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, **TOL)
+    # same result, bit for bit, on a second run (no atomics)
+    out2 = _nhwc(res, dev)
+    ops.conv2d(xa, spec, out2, res=out2, relu=True, tile=tile, splits=splits, ws=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(out2.t, out.t)
+
+
 @pytest.mark.parametrize("cin,cout,k,p,op,H", [(398, 128, 4, 1, 0, 30), (128, 128, 3, 1, 1, 30), (20, 12, 4, 1, 0, 7)])
 def test_convT(dev, cin, cout, k, p, op, H):
     g = torch.Generator().manual_seed(11 + k)

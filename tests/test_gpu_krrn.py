@@ -15,8 +15,14 @@ pytestmark = pytest.mark.gpu
 
 # relative to the tensor's max magnitude (f32, ~100 layers, different summation order)
 MAP_RTOL = 2e-4
-# pred_t absolute tolerance in metres (north_star: 1e-3 mm = 1e-6 m on T)
+# pred_t absolute tolerance in metres: north_star's 1e-3 mm, with the oracle conditioned on the
+# HIP path's kNN decisions over predicted coordinates (see test_forward_parity). Unconditioned,
+# one flipped near-tied 4th pool neighbour (measured: 1 of 2000 rows at B=2, S=120) moves
+# ~2% of the feature rows discretely and pred_t by up to ~6e-6 m; the reference itself would
+# flip the same way between its CPU and GPU runs.
 T_ATOL = 1e-6
+# per-point feature rows: the fraction whose max error stays under FEAT_RTOL of max|feat|
+FEAT_RTOL, FEAT_ROWS = 1e-3, 1.0
 
 
 def _draw_perms(N, seed):
@@ -49,29 +55,41 @@ def test_forward_parity(models, dev, B, S, N):
     torch.set_num_threads(8)
     d = make_batch(B, S, N, seed=3)
     perms = _draw_perms(N, 11)
-    tr = {}
-    ref = o(d["img_croped"], d["cloud"], d["choose"], d["cls_id"], perms=perms, trace=tr)
     out = m(d["img_croped"].to(dev), d["cloud"].to(dev), d["choose"].to(dev), d["cls_id"].to(dev),
             perms=[p.to(dev) for p in perms])
     torch.cuda.synchronize()
-    errs = {k: _rel(out[k], ref[k]) for k in ("xyz", "normal", "mask", "region")}
     plan = m.get_plan(B, S, N, True)
     fb = plan.fusion_bufs
+    # Discrete decisions made on *predicted* coordinates (the x / n pool kNNs and the 9-D idx2
+    # kNN) can flip on f32 reassociation noise; they are checked for agreement below, and the
+    # oracle is conditioned on the HIP path's choices so the arithmetic is compared like for like.
+    override = {br: fb[f"pool_{br}"].cpu() for br in ("v", "x", "n")}
+    override["idx2"] = fb["idx2"].cpu()
+    tr = {}
+    ref = o(d["img_croped"], d["cloud"], d["choose"], d["cls_id"], perms=perms, trace=tr, pool_override=override)
+    errs = {k: _rel(out[k], ref[k]) for k in ("xyz", "normal", "mask", "region")}
     exact = {}
     for k in ("idx0", "idx1", "nn1", "nn2"):
         exact[k] = float((fb[k].cpu().long() == tr[k].long()).float().mean())
-    near = {k: float((fb[k].cpu().long() == tr[k].long()).float().mean()) for k in ("idx2",)}
+    near = {k: float((fb[k].cpu().long() == tr[k].long()).float().mean())
+            for k in ("idx2", "pool_v", "pool_x", "pool_n", "pool2")}
     feat_err = _rel(plan.feat, tr["feat"][..., :1280])
+    fr = tr["feat"][..., :1280]
+    row_err = (plan.feat.cpu() - fr).abs().amax(-1) / fr.abs().max()
+    feat_rows_ok = float((row_err < FEAT_RTOL).float().mean())
     t_err = float((out["pred_t"].cpu() - ref["pred_t"]).abs().max())
-    print(f"\nB={B} S={S} N={N} map rel errs {errs} exact {exact} idx2 agree {near} feat {feat_err:.2e} "
+    print(f"\nB={B} S={S} N={N} map rel errs {errs} exact {exact} idx2 agree {near} feat {feat_err:.2e} rows ok {feat_rows_ok:.4f} "
           f"pred_t abs err {t_err:.3e} (|t| {float(ref['pred_t'].abs().max()):.3f})")
     for k, e in errs.items():
         assert e < MAP_RTOL, (k, e)
     for k, v in exact.items():
         assert v == 1.0, (k, v)
-    assert near["idx2"] > 0.97
+    for k, v in near.items():
+        assert v > 0.99, (k, v)
+    assert near["pool_v"] == 1.0 and near["pool2"] == 1.0  # these run on the exact input cloud
+    assert feat_rows_ok >= FEAT_ROWS, feat_rows_ok
     assert feat_err < 5e-3
-    assert t_err < 1e-4
+    assert t_err < T_ATOL
 
 
 def test_opt_pose_false(models, dev):
@@ -81,3 +99,31 @@ def test_opt_pose_false(models, dev):
     ref = o(d["img_croped"], d["cloud"], d["choose"], d["cls_id"], opt_pose=False)
     assert out["pred_t"] is None and out["pred_r"] is None
     assert _rel(out["xyz"], ref["xyz"]) < MAP_RTOL
+
+
+def test_forward_deterministic(models, dev):
+    """Two eager runs and a graph replay give bit-identical outputs (no races between the plan's
+    side streams, no atomics)."""
+    m, _ = models
+    B, S, N = 4, 120, 1000
+    d = make_batch(B, S, N, seed=9)
+    perms = [p.to(dev) for p in _draw_perms(N, 2)]
+    args = (d["img_croped"].to(dev), d["cloud"].to(dev), d["choose"].to(dev), d["cls_id"].to(dev))
+    o1 = {k: v.clone() for k, v in m(*args, perms=perms).items() if v is not None}
+    o2 = {k: v.clone() for k, v in m(*args, perms=perms).items() if v is not None}
+    plan = m.get_plan(B, S, N, True)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        plan.run()
+        with torch.cuda.graph(g, stream=s):
+            plan.run()
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    o3 = plan.outputs(m)
+    for k in o1:
+        assert torch.equal(o1[k], o2[k]), k
+        assert torch.equal(o1[k], o3[k]), k

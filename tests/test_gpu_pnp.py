@@ -59,25 +59,44 @@ def test_known_pose_recovery(dev):
     assert (info["inliers"].cpu().numpy() >= 200).all()
 
 
-@pytest.mark.parametrize("noise_px,cnt_tol,pose_tol", [(0.0, 0, 1e-4), (0.4, 8, 1e-2)])
+@pytest.mark.parametrize("noise_px,cnt_tol,pose_tol", [(0.0, 0, 1e-4), (0.4, 2, 2e-3)])
 def test_matches_oracle_same_subsets(dev, noise_px, cnt_tol, pose_tol):
-    # noise 0.4 px against a 1 px threshold puts many points on the threshold, where the f64
-    # rounding of the 5-point EPnP (GPU vs gcc) flips a few inlier decisions
+    """RANSAC vs the C oracle on identical subsets.
+
+    A 5-point EPnP system M (10 x 12) has a >= 2-dimensional null space, and the eigenvectors of
+    a repeated (zero) eigenvalue are defined only up to a basis choice, which differs between any
+    two eigen-solvers (GPU Jacobi vs gcc Jacobi, or vs OpenCV's). For outlier-contaminated
+    subsets the resulting hypothesis poses are therefore arbitrary on both sides (measured
+    |dR| up to 1.9 on low-count hypotheses) and not comparable. What is comparable:
+      (1) the oracle run on the GPU's selected subset reproduces its inlier count and final
+          (refined) pose -- hypothesis scoring, inlier compaction and the all-inlier EPnP;
+      (2) the GPU's RANSAC is as good as the oracle's over all subsets: which near-best subset
+          wins is chaotic on both sides (noisy crops measured: either side ahead by up to ~6%
+          on single crops), so this is asserted on the batch total."""
     B, N, S = 16, 1000, 100
     xyz, data, _, _ = _scene(B, N, S, 1, outlier_frac=0.3, noise_px=noise_px)
     R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
     torch.cuda.synchronize()
     sel = info["sel"].cpu().long()
     subs = info["subsets"].cpu()
+    H = subs.shape[1]
+    hcnt = info["workspace"].cpu()[B * H * 12:].view(torch.int32)[:B * H].view(B, H).numpy()
+    tot_gpu = tot_cpu = 0
     for b in range(B):
         s = sel[b]
         pix = data["choose"][b, 0, s]
         obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
         img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
-        Ro, to, cnt, mask, bh = opnp.pnp_ransac(obj, img, K4, subs[b].numpy(), 1.0)
-        assert abs(int(info["inliers"][b]) - cnt) <= cnt_tol, (b, int(info["inliers"][b]), cnt)
+        best_h = int(np.argmax(hcnt[b]))  # most inliers, lowest index
+        Ro, to, cnt, mask, _ = opnp.pnp_ransac(obj, img, K4, subs[b, best_h:best_h + 1].numpy(), 1.0)
+        gcnt = int(info["inliers"][b])
+        assert abs(gcnt - cnt) <= cnt_tol, (b, gcnt, cnt)
         assert np.abs(R[b].cpu().numpy() - Ro).max() < pose_tol
         assert np.abs(t[b].cpu().numpy() - to).max() < pose_tol
+        _, _, cnt_all, _, _ = opnp.pnp_ransac(obj, img, K4, subs[b].numpy(), 1.0)
+        tot_gpu += gcnt
+        tot_cpu += cnt_all
+    assert tot_gpu >= 0.99 * tot_cpu, (tot_gpu, tot_cpu)
 
 
 def test_ransac_failure_identity(dev):
