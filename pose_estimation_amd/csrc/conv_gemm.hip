@@ -61,6 +61,9 @@ struct ConvArgs {
   int Ho, Wo, osy, osx, ooy, oox;
   int relu;
   int M;
+  int tapoff[9];   // element offset of each tap: (dy*Wi + dx)*in_cs
+  unsigned cin_magic;  // ceil(2^32 / cin): k / cin == umulhi(k, cin_magic) for k * cin < 2^32
+  long long img;   // elements per input image: Hi*Wi*in_cs
   // split-K: blockIdx.y = z owns k-tiles [z*kt_per, (z+1)*kt_per) and writes its raw partial
   // sums to ws[z][M][N]; krrn_splitk_epilogue then adds the partials in z order and applies
   // the epilogue (deterministic: no atomics).
@@ -78,6 +81,7 @@ struct Cfg {
   static constexpr int AL = (BM + RPP - 1) / RPP;
   static constexpr int BL = (BN + RPP - 1) / RPP;
   static constexpr int PITCH = BK + 4;          // odd number of 16-B slots
+  static constexpr bool A_FULL = AL * RPP == BM, B_FULL = BL * RPP == BN;  // no partial staging pass
   static constexpr int A_FLOATS = BM * PITCH, B_FLOATS = BN * PITCH;
   static_assert(MI >= 1 && NI >= 1, "wave tile must be at least 32x32");
   static_assert(BK % 8 == 0, "BK multiple of 8");
@@ -107,56 +111,74 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- per-thread staging geometry -------------------------------------------------
+  // A and W are read with raw buffer loads: an out-of-range offset returns 0, so the im2col
+  // zero padding, the K tail and the M / N edges cost no branch. A's resource starts at the
+  // first image the tile touches; row offsets are 32-bit relative to it (host-checked).
   const int srow = tid / C::KQ;
   const int kq = (tid % C::KQ) * 4;  // k offset inside the tile
   const int HWg = a.Hg * a.Wg;
-  const float* a_base[AL];
-  int a_iy[AL], a_ix[AL];
-  bool a_ok[AL];
+  constexpr unsigned kOOB = 0xFFFFFFF0u;
+  const int b0 = min(m0, a.M - 1) / HWg;
+  const float* abase = a.in + (size_t)b0 * a.img + a.in_co;
+  const long long a_avail = ((long long)(a.B - b0) * a.img - a.in_co) * 4;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)abase, (short)0, (int)min(a_avail, (long long)kOOB), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.wt, (short)0, (int)min((long long)a.N * a.K * 4, (long long)kOOB), 0x00020000);
+  __shared__ int stap[16];
+  if (tid < 16) stap[tid] = tid < a.ntaps ? a.tapoff[tid] : 0;
+  unsigned a_row[AL];   // element offset of the row's (gy*s, gx*s) pixel, channel 0
+  unsigned a_vm[AL];    // bit t: tap t lands inside the image
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int r = srow + C::RPP * i;
     const int m = m0 + r;
-    a_ok[i] = (r < BM) && (m < a.M);
-    const int mm = a_ok[i] ? m : 0;
+    const bool ok = (r < BM) && (m < a.M);
+    const int mm = ok ? m : 0;
     const int b = mm / HWg;
     const int rr = mm - b * HWg;
     const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
-    a_iy[i] = gy * a.in_s;
-    a_ix[i] = gx * a.in_s;
-    a_base[i] = a.in + (size_t)b * a.Hi * a.Wi * a.in_cs + a.in_co;
+    const int iy0 = gy * a.in_s, ix0 = gx * a.in_s;
+    a_row[i] = (unsigned)((long long)(b - b0) * a.img + ((long long)iy0 * a.Wi + ix0) * a.in_cs);
+    unsigned vm = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = iy0 + a.dy[t], ix = ix0 + a.dx[t];
+      vm |= (t < a.ntaps && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi) ? (1u << t) : 0u;
+    }
+    a_vm[i] = ok ? vm : 0u;
+  }
+  unsigned b_row[BL];  // byte offset of weight row n, or kOOB
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int r = srow + C::RPP * i;
+    const int n = n0 + r;
+    b_row[i] = (r < BN && n < a.N) ? (unsigned)n * (unsigned)a.K * 4u : kOOB;
   }
   const int nkt_all = (a.K + BK - 1) / BK;
   const int kt0 = a.ws ? blockIdx.y * a.kt_per : 0;
   const int nkt = a.ws ? min(a.kt_per, nkt_all - kt0) : nkt_all;
   int kk = kt0 * BK + kq;  // absolute k of this thread's staged float4s
-  int tap = kk / a.cin;
-  int cc = kk - tap * a.cin;
+  __syncthreads();  // stap
 
   auto load_tile = [&](Stage<AL, BL>& st) {
-    int ddy = 0, ddx = 0;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t == tap) { ddy = a.dy[t]; ddx = a.dx[t]; }
-    }
-    const bool tap_ok = tap < a.ntaps;
+    // (tap, channel) of k without a divide or a data-dependent loop
+    const int tap = (int)__umulhi((unsigned)kk, a.cin_magic);
+    const int cc = kk - tap * a.cin;
+    const unsigned toff = (unsigned)(stap[min(tap, 15)] + cc);
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
-      const int iy = a_iy[i] + ddy, ix = a_ix[i] + ddx;
-      const bool ok = a_ok[i] && tap_ok && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
-      st.a[i] = ok ? *reinterpret_cast<const f32x4*>(a_base[i] + ((size_t)iy * a.Wi + ix) * a.in_cs + cc)
-                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = (a_vm[i] >> min(tap, 31)) & 1u;
+      const unsigned off = ok ? (a_row[i] + toff) * 4u : kOOB;
+      st.a[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
     }
+    const bool k_ok = kk < a.K;
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int r = srow + C::RPP * i;
-      const int n = n0 + r;
-      st.b[i] = (r < BN && n < a.N && kk < a.K) ? *reinterpret_cast<const f32x4*>(a.wt + (size_t)n * a.K + kk)
-                                                : f32x4{0.f, 0.f, 0.f, 0.f};
+      const unsigned off = k_ok ? b_row[i] + (unsigned)kk * 4u : kOOB;
+      st.b[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, off, 0, 0));
     }
     kk += BK;
-    cc += BK;
-    while (cc >= a.cin) { cc -= a.cin; ++tap; }
   };
   auto store_tile = [&](const Stage<AL, BL>& st, int buf) {
     float* As = smem + buf * (A_FLOATS + B_FLOATS);
@@ -164,12 +186,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int r = srow + C::RPP * i;
-      if (r < BM) *reinterpret_cast<f32x4*>(As + r * PITCH + kq) = st.a[i];
+      if (C::A_FULL || r < BM) *reinterpret_cast<f32x4*>(As + r * PITCH + kq) = st.a[i];
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int r = srow + C::RPP * i;
-      if (r < BN) *reinterpret_cast<f32x4*>(Bs + r * PITCH + kq) = st.b[i];
+      if (C::B_FULL || r < BN) *reinterpret_cast<f32x4*>(Bs + r * PITCH + kq) = st.b[i];
     }
   };
 
@@ -245,7 +267,22 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
       return;
     }
   }
+  // output-row table in LDS (the main loop ended on a barrier): image and output pixel of each
+  // of the tile's BM rows, computed once per row instead of once per accumulator element
   const int HWo = a.Ho * a.Wo;
+  int* s_b = reinterpret_cast<int*>(smem);
+  int* s_sp = s_b + BM;
+  int* s_b2 = s_sp + BM;
+  for (int r = tid; r < BM; r += 256) {
+    const int m = min(m0 + r, a.M - 1);
+    const int b = m / HWg;
+    const int rr = m - b * HWg;
+    const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
+    s_b[r] = b;
+    s_sp[r] = (gy * a.osy + a.ooy) * a.Wo + gx * a.osx + a.oox;
+    s_b2[r] = m / a.b2_div;
+  }
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -257,39 +294,35 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
         const float bi = a.bias ? a.bias[n] : 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * C::WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          if (m >= a.M) continue;
-          const int b = m / HWg;
-          const int rr = m - b * HWg;
-          const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
-          const int oy = gy * a.osy + a.ooy, ox = gx * a.osx + a.oox;
-          const size_t pix = ((size_t)b * a.Ho + oy) * a.Wo + ox;
+          const int row = wm * C::WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          if (m0 + row >= a.M) continue;
+          const size_t pix = (size_t)s_b[row] * HWo + s_sp[row];
           float v = acc[i][j][r] * sc + bi;
-          if (a.bias2) v += a.bias2[(size_t)(m / a.b2_div) * a.N + n];
+          if (a.bias2) v += a.bias2[(size_t)s_b2[row] * a.N + n];
           if (a.res) v += a.res[pix * a.res_cs + a.res_co + n];
           if (a.relu) v = fmaxf(v, 0.f);
           a.out[pix * a.out_cs + a.out_co + n] = v;
         }
       } else {
-        const int m = m0 + wm * C::WTM + i * 32 + frow;
-        if (m >= a.M) continue;
-        const int b = m / HWg;
-        const int rr = m - b * HWg;
-        const int gy = rr / a.Wg, gx = rr - (rr / a.Wg) * a.Wg;
-        const int oy = gy * a.osy + a.ooy, ox = gx * a.osx + a.oox;
+        const int row = wm * C::WTM + i * 32 + frow;
+        if (m0 + row >= a.M) continue;
+        const int b = s_b[row], sp = s_sp[row], b2r = s_b2[row];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int n = n0 + wn * C::WTN + j * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
           if (n >= a.n_store) continue;
           float v = acc[i][j][r] * (a.scale ? a.scale[n] : 1.f) + (a.bias ? a.bias[n] : 0.f);
-          if (a.bias2) v += a.bias2[(size_t)(m / a.b2_div) * a.N + n];
+          if (a.bias2) v += a.bias2[(size_t)b2r * a.N + n];
           if (a.relu) v = fmaxf(v, 0.f);
-          a.out[((size_t)b * a.out_cs + a.out_co + n) * HWo + (size_t)oy * a.Wo + ox] = v;
+          a.out[((size_t)b * a.out_cs + a.out_co + n) * HWo + sp] = v;
         }
       }
     }
 }
 
+}  // namespace
+
+namespace {
 // Sum of the split-K partials in z order + the conv epilogue (NHWC output). One thread per
 // (m, 4 channels).
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a, int splits) {
@@ -367,14 +400,18 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
   a.res = res; a.res_cs = res_cs; a.res_co = res_co;
   a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.Ho = Ho; a.Wo = Wo;
   a.osy = osy; a.osx = osx; a.ooy = ooy; a.oox = oox; a.relu = relu; a.M = (int)M;
-  hipStream_t s = (hipStream_t)stream;
-  if (tile == 0) {  // same rule as runtime.conv_tile
-    const long long wg128 = (long long)krrn_cdiv(a.M, 128) * krrn_cdiv(N, 128);
-    if (out_nchw) tile = wg128 >= 512 ? 1 : 3;
-    else if (N <= 32) tile = 6;
-    else if (N >= 128 && a.K >= 512 && wg128 >= 2048) tile = 4;
-    else tile = 8;
+  for (int t = 0; t < 9; ++t) a.tapoff[t] = (a.dy[t] * Wi + a.dx[t]) * in_cs;
+  a.img = (long long)Hi * Wi * in_cs;
+  a.cin_magic = (unsigned)((0x100000000ULL + cin - 1) / cin);
+  if ((long long)(a.K + 64) * cin >= 0x100000000LL) return KRRN_ESHAPE;
+  // 32-bit buffer offsets: the images one tile can touch (<= 256 rows) and the weights
+  {
+    const long long HWg = (long long)Hg * Wg;
+    const long long span = ((256 + HWg - 1) / HWg + 1) * a.img * 4;
+    if (span >= 0xFFFFFFF0LL || (long long)N * a.K * 4 >= 0xFFFFFFF0LL) return KRRN_ESHAPE;
   }
+  hipStream_t s = (hipStream_t)stream;
+  if (tile == 0) tile = out_nchw ? 3 : (N <= 32 ? 6 : 8);  // same rule as runtime.conv_tile
   a.ws = nullptr;
   a.kt_per = 0;
   if (splits > 1) {

@@ -194,16 +194,14 @@ class Plan:
 
 def conv_tile(M: int, N: int, K: int = 1024, nchw: bool = False) -> int:
     """Tile choice for krrn_conv2d_f32 from the measured menu (scratch/convbench.py on MI355X,
-    graph-replayed): 128x128x32 only for very large, deep GEMMs (>= 2048 tiles, K >= 512: the
-    S=120 head convs 103 TF, TBase conv1 104 TF); 128x32x32 with 4 waves along M for N <= 32
-    (HRNet branch 0: 22 vs 15 TF for 64x64); 64x64x32 otherwise (69 TF on layer1 3x3 vs 61)."""
-    cd = lambda a, b: (a + b - 1) // b  # noqa: E731
+    graph-replayed, buffer-load staging): 64x64x32 (4-5 waves/SIMD) is best or within 3% on
+    every wide layer (S=120 head conv 119 TF vs 121 for hipBLASLt's f32 GEMM of the same
+    shape; TBase conv1 118 TF); 128x32x32 with 4 waves along M for N <= 32 (HRNet branch 0 and
+    its transitions: 51 vs 33 TF). NCHW-output heads use 64x64x16."""
     if nchw:
-        return 1 if cd(M, 128) * cd(N, 128) >= 512 else 3
+        return 3
     if N <= 32:
         return 6
-    if N >= 128 and K >= 512 and cd(M, 128) * cd(N, 128) >= 2048:
-        return 4
     return 8
 
 

@@ -1,0 +1,64 @@
+"""Summarise a rocprofv3 --kernel-trace CSV of bench.py into per-kernel device time per step.
+
+bench.py runs (in order) an eager warm-up pass, a serial per-op profile pass (every launch on
+one stream), then the graph warm-up / timed replays (several streams, kernels overlap, so their
+rocprof durations include contention). This script finds the serial pass (the longest window
+of libkrrn_hip kernels with no overlap) and reports each kernel's isolated duration there, plus the
+wall-clock of each graph replay window.
+
+usage: python profiles/kernel_trace_summary.py <run_kernel_trace.csv> [out.json]
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"(conv_gemm_f32_kernel<[^>]*>|splitk_epilogue_kernel|\w+_kernel(<[^>]*>)?|__amd_\w+)", name)
+    return m.group(1) if m else name[:60]
+
+
+def main(path, out=None):
+    rows = list(csv.DictReader(open(path)))
+    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), int(r["Queue_Id"]))
+                 for r in rows if "anonymous namespace" in r["Kernel_Name"]), key=lambda x: x[0])
+    # mark kernels that overlap any other kernel
+    iso = []
+    end_max = -1
+    for i, (s, e, n, q) in enumerate(ks):
+        ov = s < end_max or (i + 1 < len(ks) and ks[i + 1][0] < e)
+        iso.append(not ov)
+        end_max = max(end_max, e)
+    # serial pass = longest run of consecutive isolated kernels
+    best, cur, start = (0, 0), 0, 0
+    for i, ok in enumerate(iso):
+        if ok:
+            if cur == 0:
+                start = i
+            cur += 1
+            if cur > best[1] - best[0]:
+                best = (start, i + 1)
+        else:
+            cur = 0
+    seg = ks[best[0]:best[1]]
+    per = defaultdict(lambda: [0.0, 0])
+    for s, e, n, q in seg:
+        per[n][0] += (e - s) / 1e3
+        per[n][1] += 1
+    tot = sum(v[0] for v in per.values())
+    res = {"serial_pass_kernels": len(seg), "serial_pass_busy_us": round(tot, 1),
+           "serial_pass_span_us": round((seg[-1][1] - seg[0][0]) / 1e3, 1) if seg else 0,
+           "kernels": {k: {"us": round(v[0], 1), "launches": v[1], "avg_us": round(v[0] / v[1], 2)}
+                       for k, v in sorted(per.items(), key=lambda kv: -kv[1][0])}}
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
+    print(f"serial pass: {len(seg)} kernels, busy {tot / 1e3:.2f} ms, span {res['serial_pass_span_us'] / 1e3:.2f} ms")
+    for k, v in list(res["kernels"].items())[:30]:
+        print(f"{v['us'] / 1e3:8.3f} ms x{v['launches']:4d} avg {v['avg_us']:9.2f} us  {k}")
+    return res
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
