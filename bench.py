@@ -29,48 +29,12 @@ import torch.distributed as dist  # noqa: E402
 from pose_estimation_amd import distributed as kd  # noqa: E402
 from pose_estimation_amd.config import make_config  # noqa: E402
 from pose_estimation_amd.krrn import KRRN  # noqa: E402
-from pose_estimation_amd.pose import add_pose_ops  # noqa: E402
-from pose_estimation_amd.runtime import Plan, ptr  # noqa: E402
+from pose_estimation_amd.pipeline import BatchPipeline  # noqa: E402
 from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
 
 METRIC = "crops/sec at 640×480 RGB-D, 1000 sampled pts; ADD(-S) AUC vs reference"
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-
-
-class Step:
-    """The full per-batch hot path over plan-owned static buffers."""
-
-    def __init__(self, model: KRRN, data, B: int, S: int, N: int, dev):
-        self.kp = model.get_plan(B, S, N, True)
-        kp = self.kp
-        kp.load_inputs(data["img_croped"].to(dev), data["cloud"].to(dev), data["choose"].to(dev),
-                       data["cls_id"].to(dev))
-        self.xm = data["x_map_choosed"].reshape(B, N).contiguous().to(dev)
-        self.ym = data["y_map_choosed"].reshape(B, N).contiguous().to(dev)
-        self.K4 = data["intrinsic"].contiguous().to(dev)
-        self.ext = data["extent"].double().contiguous().to(dev)
-        self.lfb = data["lfborder"].double().contiguous().to(dev)
-        self.pose_plan = Plan(dev)
-        self.R, self.t, self.inl, _ = add_pose_ops(self.pose_plan, kp.xyz, kp.choose.view(B, N), B, N, self.xm,
-                                                   self.ym, self.K4, self.ext, self.lfb, kp.seed)
-        self.pose_plan.add("krrn_rng_advance", ptr(kp.seed))
-        # per-crop pose record for the all-gather: R(9) t(3) pred_t(3) inliers(1) -> 16 f32 = 64 B
-        self.record = torch.zeros((B, 16), dtype=torch.float32, device=dev)
-        self.plans = [kp.device_perm_plan, kp.plan, self.pose_plan]
-
-    def run(self):
-        self.kp.device_perm_plan.run({})
-        self.kp.run()
-        self.pose_plan.run({})
-
-    def profile(self):
-        """Per-op device time (HIP events around every launch, eager) -> list of (op, ms)."""
-        out = []
-        for p in (self.kp.device_perm_plan, self.kp.plan, self.pose_plan):
-            env = dict(self.kp.env) if p is self.kp.plan else {}
-            out.extend(p.run_timed(env))
-        return out
 
 
 def roofline_from_profile(prof, B: int):
@@ -167,6 +131,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--cpu-baseline-s", type=float, default=15.0)
     ap.add_argument("--breakdown", default="", help="write the per-kernel breakdown JSON here")
+    ap.add_argument("--micro", type=int, default=1,
+                    help="micro-batches processed concurrently inside each step (pipeline.py)")
+    ap.add_argument("--flat", action="store_true", help="no plan side streams inside a micro-batch")
     args = ap.parse_args()
 
     rank, world, local = kd.init_from_env("nccl")
@@ -180,32 +147,21 @@ def main():
     model = model.to(dev).eval()
     model.perm_mode = "device"
     data = make_batch(B, S, N, seed=1 + rank)
-    step = Step(model, data, B, S, N, dev)
-    step.kp.seed.fill_(1000003 * (rank + 1))
+    step = BatchPipeline(model, B, S, N, dev, parts=args.micro, seed=rank, inner_streams=not args.flat)
+    step.load(data)
+    record = torch.zeros((B, kd.RECORD), dtype=torch.float32, device=dev)
 
     step.run()  # eager warm-up (compiles nothing; touches every buffer)
     torch.cuda.synchronize()
-    graph = None
     if not args.no_graph:
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            step.run()
-        torch.cuda.current_stream(dev).wait_stream(s)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step.run()
-        torch.cuda.synchronize()
+        step.capture()
 
     def one_step():
-        if graph is not None:
-            graph.replay()
-        else:
-            step.run()
+        step.step()
         if world > 1:
-            kd.pack_records(step.R, step.t, step.kp.pred_t, step.inl, out=step.record)
-            kd.gather_records(step.record)
+            for pt in step.parts:
+                kd.pack_records(pt.R, pt.t, pt.kp.pred_t, pt.inl, out=record[pt.lo:pt.hi])
+            kd.gather_records(record)
 
     for _ in range(args.warmup):
         one_step()
@@ -245,7 +201,8 @@ def main():
             "config": {"workload": f"LineMOD 'cat' batch={B}/GPU, {S}x{S} crops from 640x480 RGB-D, "
                                    f"HRNet-{args.backbone.upper()} + {N}-pt fusion + TBase, PnP-RANSAC (H=100) on GPU",
                        "batch_per_gpu": B, "crop": S, "points": N, "backbone": f"hrnet_{args.backbone}",
-                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": graph is not None},
+                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": step.graph is not None,
+                       "micro_batches": args.micro},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -46,12 +46,45 @@ extern "C" {
  *   N = computed channels (multiple of 4), n_store <= N stored; out_nchw = 1 writes
  *   out[b][out_co + n][oy][ox] with out_cs = total channels. tile (BMxBNxBK): 0 auto,
  *   1 = 128x128x16, 2 = 128x64x16, 3 = 64x64x16, 4 = 128x128x32, 5 = 256x32x16,
- *   6 = 128x32x32, 7 = 128x64x32, 8 = 64x64x32; out_nchw supports tiles 0-3 only. */
+ *   6 = 128x32x32, 7 = 128x64x32, 8 = 64x64x32; out_nchw supports tiles 0-3 only.
+ *   splits > 1 (NHWC only; N, n_store multiples of 4): split-K for small-M / deep-K layers
+ *   (the 4x4 and 8x8 HRNet branches): each of `splits` slices of the k-tiles writes raw
+ *   partial sums to workspace [splits][M][N] f32, then a second kernel sums them in slice
+ *   order and applies the epilogue (deterministic). The slice count actually used is
+ *   cdiv(nkt, cdiv(nkt, splits)) <= splits. splits = 1: workspace unused (may be NULL). */
 int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin, int Hg, int Wg,
                     int in_s, int ntaps, const int* tap_dy, const int* tap_dx, const float* wt, int N,
                     int n_store, const float* scale, const float* bias, const float* bias2, int b2_div,
                     const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co, int Ho,
-                    int Wo, int osy, int osx, int ooy, int oox, int relu, int out_nchw, int tile, void* stream);
+                    int Wo, int osy, int osx, int ooy, int oox, int relu, int out_nchw, int tile, int splits,
+                    float* workspace, void* stream);
+
+/* One problem of a grouped convolution launch: the arguments of krrn_conv2d_f32 as a struct
+ * (NHWC output only; tap_dy/tap_dx hold the first ntaps entries). */
+typedef struct krrn_conv_desc {
+  const float* in;
+  int in_cs, in_co, B, Hi, Wi, cin, Hg, Wg, in_s, ntaps;
+  int tap_dy[9];
+  int tap_dx[9];
+  const float* wt;
+  int N, n_store;
+  const float* scale;
+  const float* bias;
+  const float* bias2;
+  int b2_div;
+  const float* res;
+  int res_cs, res_co;
+  float* out;
+  int out_cs, out_co, Ho, Wo, osy, osx, ooy, oox, relu, out_nchw, splits;
+  float* workspace;
+} krrn_conv_desc;
+
+/* Up to 4 independent convolutions in ONE launch with a shared tile shape (tile 6 = 128x32x32
+ * or 8 = 64x64x32), each with its own split-K factor: the j-th conv of every HRNet branch of a
+ * HighResolutionModule (myhrnet.py:177-225: branch i is a chain of BasicBlocks on its own
+ * resolution, so the branches are independent until the fuse layer). Each problem computes
+ * exactly what krrn_conv2d_f32 would with the same descriptor. */
+int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* stream);
 
 /* k nearest neighbours without the [n, n] distance matrix.
  * Replaces gcn3d.get_neighbor_index (gcn3d.py:15-26; mode 0, drop_first = 1: topk(k+1)[1:])

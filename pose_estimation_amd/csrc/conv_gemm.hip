@@ -93,8 +93,10 @@ struct Stage {
   f32x4 b[BL];
 };
 
+// One BM x BN output tile (k-slice z of a split-K problem) of problem `a`; `bid` is the tile's
+// linear index (M-major over N tiles). Shared by the single-problem and the grouped kernels.
 template <int BM, int BN, int BK, int WGM, bool NCHW>
-__global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a) {
+__device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, const int z) {
   using C = Cfg<BM, BN, BK, WGM>;
   constexpr int MI = C::MI, NI = C::NI, AL = C::AL, BL = C::BL, PITCH = C::PITCH;
   constexpr int A_FLOATS = C::A_FLOATS, B_FLOATS = C::B_FLOATS;
@@ -105,8 +107,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
   const int wm = wave / C::WGN, wn = wave % C::WGN;
 
   const int n_tiles = (a.N + BN - 1) / BN;
-  const int m_tiles = (a.M + BM - 1) / BM;
-  const int bid = krrn_xcd_remap(blockIdx.x, m_tiles * n_tiles);
   const int tm = bid / n_tiles, tn = bid % n_tiles;
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
     b_row[i] = (r < BN && n < a.N) ? (unsigned)n * (unsigned)a.K * 4u : kOOB;
   }
   const int nkt_all = (a.K + BK - 1) / BK;
-  const int kt0 = a.ws ? blockIdx.y * a.kt_per : 0;
+  const int kt0 = a.ws ? z * a.kt_per : 0;
   const int nkt = a.ws ? min(a.kt_per, nkt_all - kt0) : nkt_all;
   int kk = kt0 * BK + kq;  // absolute k of this thread's staged float4s
   __syncthreads();  // stap
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
   // ---- epilogue -----------------------------------------------------------------------
   if constexpr (!NCHW) {
     if (a.ws) {  // split-K partial: raw sums, N-contiguous rows
-      float* w = a.ws + (size_t)blockIdx.y * a.M * a.N;
+      float* w = a.ws + (size_t)z * a.M * a.N;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -320,14 +320,41 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a)
     }
 }
 
-}  // namespace
+template <int BM, int BN, int BK, int WGM, bool NCHW>
+__global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a) {
+  const int tiles = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
+  conv_tile<BM, BN, BK, WGM, NCHW>(a, krrn_xcd_remap(blockIdx.x, tiles), blockIdx.y);
+}
 
-namespace {
+// Grouped launch: up to kMaxGroup independent problems of one tile shape in one grid (the
+// HRNet branches' convs at the same block depth: 20/36/72/144 channels at 30/15/8/4 px, each
+// alone far too small to fill 256 CUs). Problem q owns blocks [start[q], start[q+1]), split
+// into tiles[q] output tiles x splits[q] k-slices.
+constexpr int kMaxGroup = 4;
+struct ConvGroup {
+  int n;
+  int start[kMaxGroup + 1];
+  int tiles[kMaxGroup];
+  int estart[kMaxGroup + 1];  // split-K epilogue blocks
+  int splits[kMaxGroup];
+  ConvArgs p[kMaxGroup];
+};
+
+template <int BM, int BN, int BK, int WGM>
+__global__ __launch_bounds__(256, 2) void conv_group_kernel(const ConvGroup g) {
+  const int lin = krrn_xcd_remap(blockIdx.x, g.start[g.n]);
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && lin >= g.start[i]) ? 1 : 0;
+  const int local = lin - g.start[q];
+  const int tiles = g.tiles[q];
+  conv_tile<BM, BN, BK, WGM, false>(g.p[q], local % tiles, local / tiles);
+}
+
 // Sum of the split-K partials in z order + the conv epilogue (NHWC output). One thread per
 // (m, 4 channels).
-__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a, int splits) {
+__device__ __forceinline__ void splitk_epilogue(const ConvArgs& a, int splits, long long t) {
   const int nq = a.n_store >> 2;
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
   if (t >= (long long)a.M * nq) return;
   const int m = (int)(t / nq);
   const int n = (int)(t - (long long)m * nq) * 4;
@@ -351,6 +378,18 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a, 
   }
 }
 
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a, int splits) {
+  splitk_epilogue(a, splits, (long long)blockIdx.x * 256 + threadIdx.x);
+}
+
+__global__ __launch_bounds__(256) void splitk_epilogue_group_kernel(const ConvGroup g) {
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && (int)blockIdx.x >= g.estart[i]) ? 1 : 0;
+  if (g.splits[q] <= 1) return;
+  splitk_epilogue(g.p[q], g.splits[q], (long long)(blockIdx.x - g.estart[q]) * 256 + threadIdx.x);
+}
+
 template <int BM, int BN, int BK, int WGM, bool NCHW>
 int launch(const ConvArgs& a, int splits, hipStream_t s) {
   const int nwg = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
@@ -364,6 +403,79 @@ int launch(const ConvArgs& a, int splits, hipStream_t s) {
   return krrn_launch_status();
 }
 
+template <int BM, int BN, int BK, int WGM>
+int launch_group(ConvGroup& g, hipStream_t s) {
+  int blocks = 0, eblocks = 0;
+  for (int q = 0; q < g.n; ++q) {
+    const ConvArgs& a = g.p[q];
+    g.tiles[q] = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
+    g.start[q] = blocks;
+    blocks += g.tiles[q] * (a.ws ? g.splits[q] : 1);
+    g.estart[q] = eblocks;
+    if (a.ws) eblocks += (int)(((long long)a.M * (a.n_store >> 2) + 255) / 256);
+  }
+  for (int q = g.n; q <= kMaxGroup; ++q) {
+    if (q < kMaxGroup) { g.tiles[q] = 1; g.splits[q] = 1; }
+    g.start[q] = blocks;
+    g.estart[q] = eblocks;
+  }
+  hipLaunchKernelGGL((conv_group_kernel<BM, BN, BK, WGM>), dim3(blocks), dim3(256), 0, s, g);
+  if (eblocks) hipLaunchKernelGGL(splitk_epilogue_group_kernel, dim3(eblocks), dim3(256), 0, s, g);
+  return krrn_launch_status();
+}
+
+int tile_bk(int tile) { return (tile == 1 || tile == 2 || tile == 3 || tile == 5) ? 16 : 32; }
+
+// Validate one problem and pack its kernel arguments; resolves tile 0 and the effective
+// split count (every k-slice non-empty).
+int prepare(const krrn_conv_desc& d, int& tile, ConvArgs& a, int& splits) {
+  const int B = d.B, Hi = d.Hi, Wi = d.Wi, Hg = d.Hg, Wg = d.Wg, N = d.N, cin = d.cin, ntaps = d.ntaps;
+  if (!d.in || !d.wt || !d.out) return KRRN_EARG;
+  if (ntaps < 1 || ntaps > 9 || B < 1 || Hi < 1 || Wi < 1 || Hg < 1 || Wg < 1 || N < 1) return KRRN_ESHAPE;
+  if (cin < 4 || (cin & 3) || (d.in_cs & 3) || (d.in_co & 3) || d.in_co + cin > d.in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(d.in) || !krrn_aligned16(d.wt)) return KRRN_EALIGN;
+  if (d.n_store < 1 || d.n_store > N) return KRRN_ESHAPE;
+  if (d.bias2 && d.b2_div < 1) return KRRN_EARG;
+  if (!d.out_nchw && d.out_co + d.n_store > d.out_cs) return KRRN_ESHAPE;
+  if (tile < 0 || tile > 8) return KRRN_EARG;
+  const long long M = (long long)B * Hg * Wg;
+  if (M > 0x7fffffffLL) return KRRN_ESHAPE;
+  splits = d.splits;
+  if (splits < 1 || splits > 64) return KRRN_EARG;
+  if (splits > 1) {
+    if (!d.workspace || d.out_nchw) return KRRN_EARG;
+    if ((N & 3) || (d.n_store & 3)) return KRRN_EALIGN;
+    if (!krrn_aligned16(d.workspace)) return KRRN_EALIGN;
+  }
+  a.in = d.in; a.in_cs = d.in_cs; a.in_co = d.in_co; a.B = B; a.Hi = Hi; a.Wi = Wi; a.cin = cin;
+  a.Hg = Hg; a.Wg = Wg; a.in_s = d.in_s; a.ntaps = ntaps;
+  for (int t = 0; t < 9; ++t) { a.dy[t] = t < ntaps ? d.tap_dy[t] : 0; a.dx[t] = t < ntaps ? d.tap_dx[t] : 0; }
+  a.wt = d.wt; a.K = ntaps * cin; a.N = N; a.n_store = d.n_store;
+  a.scale = d.scale; a.bias = d.bias; a.bias2 = d.bias2; a.b2_div = d.b2_div > 0 ? d.b2_div : 1;
+  a.res = d.res; a.res_cs = d.res_cs; a.res_co = d.res_co;
+  a.out = d.out; a.out_cs = d.out_cs; a.out_co = d.out_co; a.Ho = d.Ho; a.Wo = d.Wo;
+  a.osy = d.osy; a.osx = d.osx; a.ooy = d.ooy; a.oox = d.oox; a.relu = d.relu; a.M = (int)M;
+  for (int t = 0; t < 9; ++t) a.tapoff[t] = (a.dy[t] * Wi + a.dx[t]) * d.in_cs;
+  a.img = (long long)Hi * Wi * d.in_cs;
+  a.cin_magic = (unsigned)((0x100000000ULL + cin - 1) / cin);
+  if ((long long)(a.K + 64) * cin >= 0x100000000LL) return KRRN_ESHAPE;
+  // 32-bit buffer offsets: the images one tile can touch (<= 256 rows) and the weights
+  const long long HWg = (long long)Hg * Wg;
+  const long long span = ((256 + HWg - 1) / HWg + 1) * a.img * 4;
+  if (span >= 0xFFFFFFF0LL || (long long)N * a.K * 4 >= 0xFFFFFFF0LL) return KRRN_ESHAPE;
+  if (tile == 0) tile = d.out_nchw ? 3 : (N <= 32 ? 6 : 8);  // same rule as runtime.conv_tile
+  a.ws = nullptr;
+  a.kt_per = 0;
+  if (splits > 1) {
+    const int nkt = krrn_cdiv(a.K, tile_bk(tile));
+    a.kt_per = krrn_cdiv(nkt, splits);
+    splits = krrn_cdiv(nkt, a.kt_per);
+    if (splits > 1) a.ws = d.workspace;
+  }
+  if (splits < 1) splits = 1;
+  return KRRN_OK;
+}
+
 }  // namespace
 
 // Tile menu (include/krrn_hip.h): 1 128x128x16, 2 128x64x16, 3 64x64x16, 4 128x128x32,
@@ -375,67 +487,51 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
                              float* out, int out_cs, int out_co, int Ho, int Wo, int osy, int osx, int ooy,
                              int oox, int relu, int out_nchw, int tile, int splits, float* workspace,
                              void* stream) {
-  if (!in || !wt || !out || !tap_dy || !tap_dx) return KRRN_EARG;
-  if (ntaps < 1 || ntaps > 9 || B < 1 || Hi < 1 || Wi < 1 || Hg < 1 || Wg < 1 || N < 1) return KRRN_ESHAPE;
-  if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
-  if (!krrn_aligned16(in) || !krrn_aligned16(wt)) return KRRN_EALIGN;
-  if (n_store < 1 || n_store > N) return KRRN_ESHAPE;
-  if (bias2 && b2_div < 1) return KRRN_EARG;
-  if (!out_nchw && out_co + n_store > out_cs) return KRRN_ESHAPE;
-  if (tile < 0 || tile > 8) return KRRN_EARG;
-  const long long M = (long long)B * Hg * Wg;
-  if (M > 0x7fffffffLL) return KRRN_ESHAPE;
-  if (splits < 1 || splits > 64) return KRRN_EARG;
-  if (splits > 1) {
-    if (!workspace || out_nchw) return KRRN_EARG;
-    if ((N & 3) || (n_store & 3)) return KRRN_EALIGN;
-    if (!krrn_aligned16(workspace)) return KRRN_EALIGN;
-  }
+  if (!tap_dy || !tap_dx) return KRRN_EARG;
+  if (ntaps < 1 || ntaps > 9) return KRRN_ESHAPE;
+  krrn_conv_desc d;
+  d.in = in; d.in_cs = in_cs; d.in_co = in_co; d.B = B; d.Hi = Hi; d.Wi = Wi; d.cin = cin;
+  d.Hg = Hg; d.Wg = Wg; d.in_s = in_s; d.ntaps = ntaps;
+  for (int t = 0; t < 9; ++t) { d.tap_dy[t] = t < ntaps ? tap_dy[t] : 0; d.tap_dx[t] = t < ntaps ? tap_dx[t] : 0; }
+  d.wt = wt; d.N = N; d.n_store = n_store; d.scale = scale; d.bias = bias; d.bias2 = bias2; d.b2_div = b2_div;
+  d.res = res; d.res_cs = res_cs; d.res_co = res_co; d.out = out; d.out_cs = out_cs; d.out_co = out_co;
+  d.Ho = Ho; d.Wo = Wo; d.osy = osy; d.osx = osx; d.ooy = ooy; d.oox = oox; d.relu = relu;
+  d.out_nchw = out_nchw; d.splits = splits; d.workspace = workspace;
   ConvArgs a;
-  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.Hi = Hi; a.Wi = Wi; a.cin = cin;
-  a.Hg = Hg; a.Wg = Wg; a.in_s = in_s; a.ntaps = ntaps;
-  for (int t = 0; t < 9; ++t) { a.dy[t] = t < ntaps ? tap_dy[t] : 0; a.dx[t] = t < ntaps ? tap_dx[t] : 0; }
-  a.wt = wt; a.K = ntaps * cin; a.N = N; a.n_store = n_store;
-  a.scale = scale; a.bias = bias; a.bias2 = bias2; a.b2_div = b2_div > 0 ? b2_div : 1;
-  a.res = res; a.res_cs = res_cs; a.res_co = res_co;
-  a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.Ho = Ho; a.Wo = Wo;
-  a.osy = osy; a.osx = osx; a.ooy = ooy; a.oox = oox; a.relu = relu; a.M = (int)M;
-  for (int t = 0; t < 9; ++t) a.tapoff[t] = (a.dy[t] * Wi + a.dx[t]) * in_cs;
-  a.img = (long long)Hi * Wi * in_cs;
-  a.cin_magic = (unsigned)((0x100000000ULL + cin - 1) / cin);
-  if ((long long)(a.K + 64) * cin >= 0x100000000LL) return KRRN_ESHAPE;
-  // 32-bit buffer offsets: the images one tile can touch (<= 256 rows) and the weights
-  {
-    const long long HWg = (long long)Hg * Wg;
-    const long long span = ((256 + HWg - 1) / HWg + 1) * a.img * 4;
-    if (span >= 0xFFFFFFF0LL || (long long)N * a.K * 4 >= 0xFFFFFFF0LL) return KRRN_ESHAPE;
-  }
+  int sp = 1;
+  const int st = prepare(d, tile, a, sp);
+  if (st != KRRN_OK) return st;
   hipStream_t s = (hipStream_t)stream;
-  if (tile == 0) tile = out_nchw ? 3 : (N <= 32 ? 6 : 8);  // same rule as runtime.conv_tile
-  a.ws = nullptr;
-  a.kt_per = 0;
-  if (splits > 1) {
-    // every split gets kt_per k-tiles of the chosen tile's BK; the host sized `splits` so
-    // that none is empty (splits <= cdiv(K, BK))
-    const int bk = (tile == 1 || tile == 2 || tile == 3 || tile == 5) ? 16 : 32;
-    const int nkt = krrn_cdiv(a.K, bk);
-    a.kt_per = krrn_cdiv(nkt, splits);
-    splits = krrn_cdiv(nkt, a.kt_per);
-    if (splits > 1) a.ws = workspace;
-  }
   if (out_nchw) {
     if (tile == 1 || tile == 4) return launch<128, 128, 16, 2, true>(a, 1, s);
     if (tile == 2 || tile == 7) return launch<128, 64, 16, 2, true>(a, 1, s);
     return launch<64, 64, 16, 2, true>(a, 1, s);
   }
   switch (tile) {
-    case 1: return launch<128, 128, 16, 2, false>(a, splits, s);
-    case 2: return launch<128, 64, 16, 2, false>(a, splits, s);
-    case 3: return launch<64, 64, 16, 2, false>(a, splits, s);
-    case 4: return launch<128, 128, 32, 2, false>(a, splits, s);
-    case 5: return launch<256, 32, 16, 4, false>(a, splits, s);
-    case 6: return launch<128, 32, 32, 4, false>(a, splits, s);
-    case 7: return launch<128, 64, 32, 2, false>(a, splits, s);
-    default: return launch<64, 64, 32, 2, false>(a, splits, s);
+    case 1: return launch<128, 128, 16, 2, false>(a, sp, s);
+    case 2: return launch<128, 64, 16, 2, false>(a, sp, s);
+    case 3: return launch<64, 64, 16, 2, false>(a, sp, s);
+    case 4: return launch<128, 128, 32, 2, false>(a, sp, s);
+    case 5: return launch<256, 32, 16, 4, false>(a, sp, s);
+    case 6: return launch<128, 32, 32, 4, false>(a, sp, s);
+    case 7: return launch<128, 64, 32, 2, false>(a, sp, s);
+    default: return launch<64, 64, 32, 2, false>(a, sp, s);
   }
+}
+
+KRRN_API int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* stream) {
+  if (!descs) return KRRN_EARG;
+  if (n < 1 || n > kMaxGroup) return KRRN_ESHAPE;
+  if (tile != 6 && tile != 8) return KRRN_EARG;
+  ConvGroup g;
+  g.n = n;
+  for (int q = 0; q < n; ++q) {
+    if (descs[q].out_nchw) return KRRN_EARG;
+    int t = tile;
+    const int st = prepare(descs[q], t, g.p[q], g.splits[q]);
+    if (st != KRRN_OK) return st;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (tile == 6) return launch_group<128, 32, 32, 4>(g, s);
+  return launch_group<64, 64, 32, 2>(g, s);
 }

@@ -24,7 +24,7 @@ static inline int krrn_launch_status() {
 
 static inline bool krrn_aligned16(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
 
-static inline int krrn_cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ static inline int krrn_cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): consecutive logical tiles land on the same XCD so that tiles that share

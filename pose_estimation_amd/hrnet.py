@@ -20,6 +20,7 @@ pad channels are exactly zero and the packed weights map logical -> physical cha
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -28,7 +29,12 @@ import torch.nn as nn
 from . import ops
 from .config import load_hrnet_spec
 from .ops import Act, pad4
-from .runtime import Plan, add_conv, ptr
+from .runtime import add_conv_group, Plan, add_conv, ptr
+
+# HRNet branch convs as per-branch chains on plan streams (default: measured 23.5 ms/step) or
+# as grouped launches, one per block depth (KRRN_HR_GROUP=1: 25.4 ms/step; the grouped launch
+# is bound by its slowest member and loses the cross-branch overlap of the streams)
+HR_GROUP = os.environ.get("KRRN_HR_GROUP", "0") == "1"
 
 BN_MOMENTUM = 0.1
 
@@ -224,6 +230,36 @@ class _Builder:
                      out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=osy, osx=osx, ooy=ooy,
                      oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag)
 
+    def conv_problem(self, x: Act, conv: nn.Module, bn: Optional[nn.Module], res: Optional[Act] = None,
+                     relu: bool = False) -> Tuple[dict, Act]:
+        """A stride-1 / stride-2 conv as one problem of a grouped launch (no emission)."""
+        spec = ops.make_conv(conv, bn, self.dev, cin_p=x.cp)
+        self.specs.append(spec)
+        Ho, Wo = ops.conv_out_hw(spec, x.H, x.W)
+        out = self.act(Ho, Wo, spec.cout)
+        np_ = pad4(spec.cout)
+        pr = dict(x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=Ho, Wg=Wo,
+                  in_s=spec.stride, taps=spec.taps[0], wt=ptr(spec.wt[0]), N=np_, n_store=np_,
+                  scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(res.t) if res is not None else None,
+                  res_cs=res.cs if res is not None else 0, res_co=res.co if res is not None else 0,
+                  out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=Ho, Wo=Wo, relu=relu, cin=spec.cin,
+                  cout=spec.cout)
+        return pr, out
+
+    def branches_grouped(self, xs: List[Act], m: "HighResolutionModule") -> List[Act]:
+        """All branches of a module, block by block: the j-th conv of every branch in ONE grouped
+        launch (myhrnet.py:226-231 runs branch i's BasicBlocks on x[i]; nothing couples them)."""
+        cur = list(xs)
+        for bi in range(len(m.branches[0])):
+            blks = [m.branches[i][bi] for i in range(m.num_branches)]
+            probs, hs = zip(*[self.conv_problem(cur[i], b.conv1, b.bn1, relu=True) for i, b in enumerate(blks)])
+            add_conv_group(self.plan, list(probs), tag="hr_branch_conv1")
+            probs, ys = zip(*[self.conv_problem(hs[i], b.conv2, b.bn2, res=cur[i], relu=True)
+                              for i, b in enumerate(blks)])
+            add_conv_group(self.plan, list(probs), tag="hr_branch_conv2")
+            cur = list(ys)
+        return cur
+
     def resize(self, x: Act, out: Act, add: Optional[Act] = None, align: bool = False, relu: bool = False):
         assert x.cp == out.cp
         self.plan.add("krrn_resize_bilinear_f32", ptr(x.t), x.B, x.H, x.W, x.cs, x.co, x.cp, ptr(out.t), out.H,
@@ -253,14 +289,19 @@ class _Builder:
         plan = self.plan
         nb = m.num_branches
         side = list(range(1, nb))
-        ys = []
-        plan.fork(side)
-        for i, x in enumerate(xs):
-            with plan.on_stream(i):
-                for blk in m.branches[i]:
-                    x = self.basic(x, blk)
-            ys.append(x)
-        plan.join(side)
+        groupable = HR_GROUP and 1 < nb <= 4 and all(len(m.branches[i]) == len(m.branches[0]) for i in range(nb)) and all(
+            isinstance(b, BasicBlock) and b.downsample is None for br in m.branches for b in br)
+        if groupable:
+            ys = self.branches_grouped(xs, m)
+        else:
+            ys = []
+            plan.fork(side)
+            for i, x in enumerate(xs):
+                with plan.on_stream(i):
+                    for blk in m.branches[i]:
+                        x = self.basic(x, blk)
+                ys.append(x)
+            plan.join(side)
         if nb == 1:
             return ys
         fused = []

@@ -1,0 +1,144 @@
+"""Fixed-shape batch pipeline: KRRN forward + get_pose as one graph-capturable step.
+
+This is the eval loop of tools/trainer.py:440-480 (forward, then get_pose per crop) for a
+whole batch, with the device-side randomness the reference draws on the host (Pool_layer
+randperms, the 256-point PnP subset, the RANSAC hypotheses), so a step needs no host sync and
+can be captured once into a hipGraph and replayed.
+
+Micro-batch concurrency (parts > 1): the batch is split into `parts` equal slices, each with
+its own compiled plan, run side by side on their own streams inside the same step. The HRNet
+low-resolution branches, the GCN levels and PnP are latency-bound (small grids, long
+dependency chains) while the S=120 head convs are MFMA-bound; running two slices at once
+lets one slice's latency-bound phases fill the CUs the other's big GEMMs leave idle. Every
+crop of the batch is still processed exactly once per step, with the same per-crop math.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from .krrn import KRRN, KRRNPlan
+from .pose import add_pose_ops
+from .runtime import Plan, ptr
+
+
+@dataclass
+class _Part:
+    kp: KRRNPlan
+    pose: Plan
+    xm: torch.Tensor
+    ym: torch.Tensor
+    K4: torch.Tensor
+    ext: torch.Tensor
+    lfb: torch.Tensor
+    R: torch.Tensor
+    t: torch.Tensor
+    inl: torch.Tensor
+    lo: int
+    hi: int
+
+
+class BatchPipeline:
+    def __init__(self, model: KRRN, B: int, S: int, N: int, device, parts: int = 1, seed: int = 0,
+                 inner_streams: bool = True):
+        if B % parts:
+            raise ValueError(f"batch {B} not divisible into {parts} parts")
+        self.B, self.S, self.N, self.device = B, S, N, torch.device(device)
+        b = B // parts
+        self.parts: List[_Part] = []
+        for p in range(parts):
+            with torch.no_grad():
+                kp = KRRNPlan(model, b, S, N, True, self.device)
+            kp.seed.fill_(1000003 * (seed + 1) + 7919 * p)
+            dev = self.device
+            xm = torch.zeros((b, N), device=dev)
+            ym = torch.zeros((b, N), device=dev)
+            K4 = torch.zeros((b, 4), device=dev)
+            ext = torch.zeros((b, 3), dtype=torch.float64, device=dev)
+            lfb = torch.zeros((b, 3), dtype=torch.float64, device=dev)
+            pose = Plan(dev)
+            R, t, inl, _ = add_pose_ops(pose, kp.xyz, kp.choose.view(b, N), b, N, xm, ym, K4, ext, lfb, kp.seed)
+            pose.add("krrn_rng_advance", ptr(kp.seed))
+            self.parts.append(_Part(kp, pose, xm, ym, K4, ext, lfb, R, t, inl, p * b, (p + 1) * b))
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)] if parts > 1 else []
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.inner_streams = inner_streams
+
+    # -- inputs / outputs ------------------------------------------------------------------
+    def load(self, data: Dict[str, torch.Tensor]):
+        """Copy one batch (PoseDataset item keys, batchdataset.py:730-771) into the static
+        buffers. Host tensors are copied asynchronously on the current stream."""
+        N = self.N
+        for pt in self.parts:
+            sl = slice(pt.lo, pt.hi)
+            b = pt.hi - pt.lo
+            pt.kp.load_inputs(data["img_croped"][sl].to(self.device), data["cloud"][sl].to(self.device),
+                              data["choose"][sl].to(self.device), data["cls_id"][sl].to(self.device))
+            pt.xm.copy_(data["x_map_choosed"][sl].reshape(b, N), non_blocking=True)
+            pt.ym.copy_(data["y_map_choosed"][sl].reshape(b, N), non_blocking=True)
+            pt.K4.copy_(data["intrinsic"][sl].reshape(b, 4), non_blocking=True)
+            pt.ext.copy_(data["extent"][sl].reshape(b, 3), non_blocking=True)
+            pt.lfb.copy_(data["lfborder"][sl].reshape(b, 3), non_blocking=True)
+
+    def results(self) -> Dict[str, torch.Tensor]:
+        """R [B,3,3], t [B,3] (PnP), pred_t [B,3] (TBase), inliers [B] of the last step."""
+        cat = lambda xs: xs[0] if len(xs) == 1 else torch.cat(xs)  # noqa: E731
+        return {"R": cat([p.R for p in self.parts]), "t": cat([p.t for p in self.parts]),
+                "pred_t": cat([p.kp.pred_t for p in self.parts]), "inliers": cat([p.inl for p in self.parts])}
+
+    def plans(self):
+        """(plan, env) pairs of every launch list, in step order (per part)."""
+        out = []
+        for pt in self.parts:
+            out += [(pt.kp.device_perm_plan, {}), (pt.kp.plan, pt.kp.env), (pt.pose, {})]
+        return out
+
+    # -- execution -------------------------------------------------------------------------
+    def _run_part(self, pt: _Part, serial: bool):
+        pt.kp.device_perm_plan.run({}, serial=serial)
+        pt.kp.plan.run(pt.kp.env, serial=serial)
+        pt.pose.run({}, serial=serial)
+
+    def run(self, serial: bool = False):
+        """Enqueue one step on the current stream (micro-batches fork onto their streams and
+        join back)."""
+        if not self.streams or serial:
+            for pt in self.parts:
+                self._run_part(pt, serial)
+            return
+        main = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(main)
+        for pt, s in zip(self.parts, self.streams):
+            with torch.cuda.stream(s):
+                self._run_part(pt, not self.inner_streams)
+        for s in self.streams:
+            main.wait_stream(s)
+
+    def capture(self):
+        """Warm up once, then capture one step into a hipGraph."""
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self.run()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.run()
+        torch.cuda.synchronize(self.device)
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.run()
+
+    def profile(self):
+        """Per-op device time of one serial step (HIP events around every launch)."""
+        out = []
+        for p, env in self.plans():
+            out.extend(p.run_timed(dict(env)))
+        return out

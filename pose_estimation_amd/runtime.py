@@ -40,6 +40,16 @@ _lib.register("krrn_pnp_ransac_f32", [P, I, P, I, P, I, P, P, P, P, P, P, I, F, 
 _lib.register("krrn_randperm_i32", [P, U, I, I, I, P, P])
 _lib.register("krrn_ransac_subsets", [P, U, I, I, I, P, P])
 _lib.register("krrn_rng_advance", [P, P])
+_lib.register("krrn_conv2d_group_f32", [P, I, I, P])
+
+
+class ConvDesc(ctypes.Structure):
+    """krrn_conv_desc (include/krrn_hip.h)."""
+    _fields_ = [("in_", P), ("in_cs", I), ("in_co", I), ("B", I), ("Hi", I), ("Wi", I), ("cin", I), ("Hg", I),
+                ("Wg", I), ("in_s", I), ("ntaps", I), ("tap_dy", I * 9), ("tap_dx", I * 9), ("wt", P), ("N", I),
+                ("n_store", I), ("scale", P), ("bias", P), ("bias2", P), ("b2_div", I), ("res", P), ("res_cs", I),
+                ("res_co", I), ("out", P), ("out_cs", I), ("out_co", I), ("Ho", I), ("Wo", I), ("osy", I),
+                ("osx", I), ("ooy", I), ("oox", I), ("relu", I), ("out_nchw", I), ("splits", I), ("workspace", P)]
 
 STREAM = "__stream__"
 
@@ -116,20 +126,22 @@ class Plan:
         self.cur = 0
         self.nstreams = 1
         self._side: List[torch.cuda.Stream] = []
-        self._scratch: Dict[int, torch.Tensor] = {}
+        self._scratch: Dict[Tuple[int, int], torch.Tensor] = {}
 
     def buf(self, shape, dtype=torch.float32, zero: bool = True) -> torch.Tensor:
         t = (torch.zeros if zero else torch.empty)(tuple(shape), dtype=dtype, device=self.device)
         self.buffers.append(t)
         return t
 
-    def scratch(self, nfloats: int) -> torch.Tensor:
+    def scratch(self, nfloats: int, slot: int = 0) -> torch.Tensor:
         """A workspace for the current stream (ops on one stream run in order, so they can share
-        it; a larger request allocates a larger one, earlier ops keep theirs)."""
-        ws = self._scratch.get(self.cur)
+        it; a larger request allocates a larger one, earlier ops keep theirs). `slot` separates
+        the problems of one grouped launch, which run concurrently."""
+        key = (self.cur, slot)
+        ws = self._scratch.get(key)
         if ws is None or ws.numel() < nfloats:
             ws = self.buf((max(nfloats, 1 << 20),), zero=False)
-            self._scratch[self.cur] = ws
+            self._scratch[key] = ws
         return ws
 
     def add(self, name: str, *args, meta: Optional[dict] = None):
@@ -254,3 +266,49 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
              int(relu), int(nchw), tile, splits, ptr(ws),
              meta=dict(kernel=CONV_KERNELS[tile] + (",nchw" if nchw else "") + (",splitk" if splits > 1 else ""),
                        flops=flops, tag=tag, M=M, N=N, K=K, splits=splits))
+
+
+GROUP_TILE = int(os.environ.get("KRRN_GROUP_TILE", "6"))
+
+
+def conv_desc(*, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_store, scale, bias, res=None,
+              res_cs=0, res_co=0, out, out_cs, out_co, Ho, Wo, osy=1, osx=1, ooy=0, oox=0, relu=False,
+              splits=1, ws=None) -> ConvDesc:
+    d = ConvDesc()
+    d.in_, d.in_cs, d.in_co, d.B, d.Hi, d.Wi, d.cin, d.Hg, d.Wg, d.in_s = x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s
+    d.ntaps = len(taps)
+    for i, (dy, dx) in enumerate(taps):
+        d.tap_dy[i], d.tap_dx[i] = dy, dx
+    d.wt, d.N, d.n_store, d.scale, d.bias, d.bias2, d.b2_div = wt, N, n_store, scale, bias, P(0), 1
+    d.res = res if res is not None else P(0)
+    d.res_cs, d.res_co = res_cs, res_co
+    d.out, d.out_cs, d.out_co, d.Ho, d.Wo = out, out_cs, out_co, Ho, Wo
+    d.osy, d.osx, d.ooy, d.oox, d.relu, d.out_nchw = osy, osx, ooy, oox, int(relu), 0
+    d.splits, d.workspace = splits, (ws if ws is not None else P(0))
+    return d
+
+
+def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str = "group"):
+    """One krrn_conv2d_group_f32 launch over up to 4 independent convs (dicts of conv_desc
+    keyword arguments plus 'cin' / 'cout' logical channels for the FLOP count)."""
+    tile = GROUP_TILE if tile is None else tile
+    n = len(problems)
+    arr = (ConvDesc * n)()
+    flops = 0.0
+    nsplit = 1
+    shapes = []
+    for q, pr in enumerate(problems):
+        pr = dict(pr)
+        cin, cout = pr.pop("cin"), pr.pop("cout")
+        M = pr["B"] * pr["Hg"] * pr["Wg"]
+        K = pr["cin_p"] * len(pr["taps"])
+        sp = conv_splits(M, pr["N"], K, tile)
+        ws = ptr(plan.scratch(sp * M * pr["N"], slot=q)) if sp > 1 else None
+        arr[q] = conv_desc(**pr, splits=sp, ws=ws)
+        flops += 2.0 * cin * cout * len(pr["taps"]) * M
+        nsplit = max(nsplit, sp)
+        shapes.append((M, pr["N"], K, sp))
+    plan.buffers.append(arr)
+    plan.add("krrn_conv2d_group_f32", ctypes.cast(arr, P), n, tile,
+             meta=dict(kernel=f"conv_group<{','.join(map(str, TILE_SHAPES[tile]))}>", flops=flops, tag=tag,
+                       M=shapes[0][0], N=shapes[0][1], K=shapes[0][2], splits=nsplit, shapes=shapes))

@@ -137,3 +137,43 @@ def test_gemm_bias2(dev):
     ops.gemm(a.to(dev), K, 0, M, spec, out, N, 0, relu=True, bias2=b2.to(dev), b2_div=per)
     torch.cuda.synchronize()
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("tile", [6, 8])
+def test_conv_group_matches_single(dev, tile):
+    """krrn_conv2d_group_f32 over the four HRNet-W18 branch shapes (incl. split-K members) gives
+    bit-identical results to the same problems launched one by one."""
+    import ctypes
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, add_conv_group, conv_splits, Plan, ptr
+    g = torch.Generator().manual_seed(5)
+    shapes = [(20, 30), (36, 15), (72, 8), (144, 4)]
+    B = 16
+    plan = Plan(dev)
+    probs, outs, refs = [], [], []
+    for c, H in shapes:
+        conv = nn.Conv2d(c, c, 3, 1, 1, bias=False)
+        with torch.no_grad():
+            conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+        bn = _bn(c, g)
+        x = torch.randn(B, c, H, H, generator=g)
+        res = torch.randn(B, c, H, H, generator=g)
+        spec = ops.make_conv(conv, bn, dev)
+        xa, ra = _nhwc(x, dev), _nhwc(res, dev)
+        out = ops.new_act(B, H, H, c, dev)
+        ref = ops.new_act(B, H, H, c, dev)
+        M, K = B * H * H, spec.cin_p * 9
+        sp = conv_splits(M, ops.pad4(c), K, tile)
+        ws = torch.empty(max(1, sp) * M * ops.pad4(c), device=dev)
+        ops.conv2d(xa, spec, ref, res=ra, relu=True, tile=tile, splits=sp, ws=ws)
+        probs.append(dict(x=ptr(xa.t), x_cs=xa.cs, x_co=0, B=B, Hi=H, Wi=H, cin_p=spec.cin_p, Hg=H, Wg=H, in_s=1,
+                          taps=spec.taps[0], wt=ptr(spec.wt[0]), N=ops.pad4(c), n_store=ops.pad4(c),
+                          scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(ra.t), res_cs=ra.cs, res_co=0,
+                          out=ptr(out.t), out_cs=out.cs, out_co=0, Ho=H, Wo=H, relu=True, cin=c, cout=c))
+        outs.append(out)
+        refs.append((ref, spec, xa, ra))
+    add_conv_group(plan, probs, tile=tile)
+    plan.run({})
+    torch.cuda.synchronize()
+    for out, (ref, *_keep) in zip(outs, refs):
+        assert torch.equal(out.t, ref.t)
