@@ -86,6 +86,16 @@ typedef struct krrn_conv_desc {
  * exactly what krrn_conv2d_f32 would with the same descriptor. */
 int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* stream);
 
+/* 3x3 stride-1 pad-1 convolution by fused Winograd F(2x2, 3x3) (the head / last_layer /
+ * deconv-BasicBlock convs: krrn.py:46-84, myhrnet.py:324-346; cuDNN / MIOpen use the same
+ * algorithm for these f32 convs). U = G g G^T are the transformed weights, [16][N][cin] f32
+ * (element xi = 4u + v of the 4x4 transform), computed once per plan; epilogue as
+ * krrn_conv2d_f32: out = act(scale[n] * conv + bias[n] (+ res)). NHWC in/out with channel
+ * stride / offset; cin multiple of 4, in 8-byte aligned, U 16-byte aligned. */
+int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* U,
+                          int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
+                          int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
+
 /* k nearest neighbours without the [n, n] distance matrix.
  * Replaces gcn3d.get_neighbor_index (gcn3d.py:15-26; mode 0, drop_first = 1: topk(k+1)[1:])
  * and gcn3d.get_nearest_index (gcn3d.py:29-38; mode 1, k = 1, drop_first = 0).

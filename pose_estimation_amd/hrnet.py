@@ -213,8 +213,25 @@ class _Builder:
         if out is None:
             out = self.act(Ho, Wo, spec.cout)
         assert (out.H, out.W) == (Ho, Wo) and out.cp >= pad4(spec.cout)
-        self.emit_conv(x, spec, out, res, relu)
+        if ops.wino_eligible(spec, x.B * Ho * Wo) and x.cs % 2 == 0 and x.co % 2 == 0:
+            U = ops.wino_weights(conv, self.dev, cin_map=cin_map, cin_p=x.cp)
+            self.specs.append(U)
+            self.emit_wino(x, spec, U, out, res, relu)
+        else:
+            self.emit_conv(x, spec, out, res, relu)
         return out
+
+    def emit_wino(self, x: Act, spec, U: torch.Tensor, out: Act, res: Optional[Act], relu: bool,
+                  tag: str = "conv"):
+        np_ = pad4(spec.cout)
+        M = x.B * out.H * out.W
+        self.plan.add("krrn_conv3x3_wino_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(U), np_, np_,
+                      ptr(spec.scale), ptr(spec.bias), ptr(res.t) if res is not None else ptr(None),
+                      res.cs if res is not None else 0, res.co if res is not None else 0, ptr(out.t), out.cs,
+                      out.co, int(relu),
+                      meta=dict(kernel="wino_f23<32,32,16>", flops=2.0 * spec.cin * spec.cout * 9 * M, tag=tag + "_wino",
+                                M=M, N=np_, K=spec.cin_p * 9,
+                                mfma_flops=2.0 * 16 * spec.cin_p * np_ * x.B * ((out.H + 1) // 2) * ((out.W + 1) // 2)))
 
     def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         np_ = pad4(spec.cout)

@@ -202,6 +202,34 @@ def make_conv(conv: torch.nn.Conv2d, bn: Optional[torch.nn.Module], device, cin_
     return ConvSpec([wt], [taps], [(0, 0)], scale, bias, cin_p, cout, s, "conv", k, pad, len(cin_map))
 
 
+# Winograd F(2x2, 3x3) weight transform G (Lavin & Gray 2016): U = G g G^T
+WINO_G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]], dtype=torch.float64)
+
+
+def wino_weights(conv: torch.nn.Conv2d, device, cin_map: Optional[List[int]] = None,
+                 cin_p: Optional[int] = None) -> torch.Tensor:
+    """[cout, cin, 3, 3] -> U [16][pad4(cout)][cin_p] f32 (xi = 4u + v), transformed in f64."""
+    w = conv.weight.detach().cpu().double()
+    cout, cin = w.shape[:2]
+    if cin_map is None:
+        cin_map = list(range(cin))
+    cin_p = pad4(max(cin_map) + 1) if cin_p is None else cin_p
+    u = torch.einsum("ui,ncij,vj->uvnc", WINO_G, w, WINO_G)  # [4, 4, cout, cin]
+    out = torch.zeros(16, pad4(cout), cin_p, dtype=torch.float64)
+    out[:, :cout, torch.tensor(cin_map, dtype=torch.long)] = u.reshape(16, cout, cin)
+    return out.float().contiguous().to(device)
+
+
+def wino_eligible(spec: ConvSpec, M: int) -> bool:
+    """Fused Winograd for the wide stride-1 3x3 convs (>= 32 channels in and out, >= 32k output
+    pixels); the narrow HRNet branches stay on the implicit GEMM (latency-bound there)."""
+    import os
+    if os.environ.get("KRRN_WINO", "1") == "0":
+        return False
+    return (spec.kind == "conv" and spec.ksize == 3 and spec.stride == 1 and spec.pad == 1
+            and spec.cin_p >= 32 and spec.cout >= 32 and M >= 32768)
+
+
 def make_convT(convT: torch.nn.ConvTranspose2d, bn: Optional[torch.nn.Module], device,
                cin_map: Optional[List[int]] = None, cin_p: Optional[int] = None) -> ConvSpec:
     """Stride-2 ConvTranspose2d as four parity-class convolutions.

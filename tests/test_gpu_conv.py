@@ -177,3 +177,35 @@ def test_conv_group_matches_single(dev, tile):
     torch.cuda.synchronize()
     for out, (ref, *_keep) in zip(outs, refs):
         assert torch.equal(out.t, ref.t)
+
+
+@pytest.mark.parametrize("cin,cout,H,W,co", [(128, 128, 30, 30, 0), (64, 72, 17, 23, 4), (272, 272, 15, 15, 0),
+                                             (36, 40, 9, 8, 8)])
+def test_conv3x3_winograd(dev, cin, cout, H, W, co):
+    """Fused Winograd F(2x2,3x3) (odd sizes, channel-offset input, residual) vs torch fp32 conv."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, ptr
+    g = torch.Generator().manual_seed(cin + cout + H)
+    B = 3
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+        conv.bias.copy_(0.1 * torch.randn(cout, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, W, generator=g)
+    res = torch.randn(B, cout, H, W, generator=g)
+    ref = torch.relu(bn(conv(x)) + res).detach()
+    cs = ops.pad4(cin) + co + 4
+    xa = _nhwc(x, dev, cs=cs, co=co)
+    spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
+    U = ops.wino_weights(conv, dev, cin_p=ops.pad4(cin))
+    ra = _nhwc(res, dev)
+    out = ops.new_act(B, H, W, cout, dev, cs=ops.pad4(cout) + 4)
+    np_ = ops.pad4(cout)
+    _lib.check(_lib.lib().krrn_conv3x3_wino_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U), np_, np_,
+                                                ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
+                                                out.cs, 0, 1, P(torch.cuda.current_stream().cuda_stream)), "wino")
+    torch.cuda.synchronize()
+    got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, **TOL)
+    assert torch.count_nonzero(out.t[..., np_:]).item() == 0
