@@ -91,7 +91,7 @@ int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* st
  * algorithm for these f32 convs). U = G g G^T are the transformed weights, [16][N][cin] f32
  * (element xi = 4u + v of the 4x4 transform), computed once per plan; epilogue as
  * krrn_conv2d_f32: out = act(scale[n] * conv + bias[n] (+ res)). NHWC in/out with channel
- * stride / offset; cin multiple of 4, in 8-byte aligned, U 16-byte aligned. */
+ * stride / offset; cin multiple of 4, U 16-byte aligned. */
 int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* U,
                           int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                           int res_co, float* out, int out_cs, int out_co, int relu, void* stream);

@@ -14,26 +14,26 @@
 // (Lavin & Gray 2016). The 16 products per tile replace 36 multiply-adds of the direct
 // conv: 2.25x fewer MFMA flops. Neither V nor M ever leaves the CU.
 //
-// Block = 32 tiles x 32 output channels, 256 threads = 4 waves, wave (wt, wn) owning a
-// 16-tile x 16-channel sub-block for ALL 16 components (16 accumulators of
-// v_mfma_f32_16x16x4_f32), so the output transform is lane-local: lane l holds, for each of
-// its 4 (tile, n) positions, the 16 values M[xi] in the same register slot of the 16
-// accumulators. Input channels stream in chunks of 16: each thread builds V for one
-// (tile, channel pair) from a 4x4 patch read with raw buffer loads (out-of-image pixels
-// return 0: the conv's zero padding), weights for the chunk are staged [xi][n][c]; both
-// k-contiguous in LDS (pitch 20 floats = 5 x 16 B: conflict-free ds_read_b128), one
-// ds_read_b128 per operand feeding 4 MFMAs (k permuted inside the 16-channel chunk). The
-// next chunk's global loads are in flight while the current chunk's 64 MFMAs run.
+// Block = 32 tiles x 64 output channels, 256 threads = 4 waves; wave w owns components
+// xi = 4w .. 4w+3 over the whole 32 x 64 block (2 x v_mfma_f32_32x32x2_f32 n-blocks each, 128
+// accumulator registers). Input channels stream in chunks of 8: thread (tile, channel) builds
+// the 16 V values from its 4x4 patch (raw buffer loads, out-of-image pixels return 0 = the
+// conv's zero padding; patch offsets precomputed once), weights are staged [xi][n][c]; both
+// k-contiguous in LDS (pitch 12 floats = 3 x 16 B: conflict-free ds_read_b128) so one
+// ds_read_b128 per operand feeds 4 MFMAs. 73.5 KB of LDS -> 2 blocks per CU, so one block's
+// staging overlaps the other's MFMAs; the next chunk's global loads are in flight during the
+// current chunk's MFMAs. The output transform needs all 16 components of a (tile, channel):
+// M goes through LDS once per 32-channel n-block at the end.
 #include "krrn_common.h"
 
 namespace {
 
-constexpr int kWT = 32;     // tiles per block
-constexpr int kWN = 32;     // output channels per block
-constexpr int kWC = 16;     // input channels per chunk
-constexpr int kWP = kWC + 4;  // LDS row pitch (floats)
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int kWT = 32;       // tiles per block
+constexpr int kWN = 64;       // output channels per block
+constexpr int kWC = 8;        // input channels per chunk
+constexpr int kWP = kWC + 4;  // LDS row pitch (floats): 3 x 16 B
+constexpr int kMP = 33;       // output-staging pitch
+constexpr unsigned kWOOB = 0xFFFF0000u;  // > any valid offset, and + channel offsets stays > it
 
 struct WinoArgs {
   const float* in;
@@ -53,31 +53,29 @@ struct WinoArgs {
 };
 
 __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float As[16 * kWT * kWP];
-  __shared__ __attribute__((aligned(16))) float Bs[16 * kWN * kWP];
+  __shared__ __attribute__((aligned(16))) float smem[16 * (kWT + kWN) * kWP];
+  float* As = smem;                   // [xi][tile][c]
+  float* Bs = smem + 16 * kWT * kWP;  // [xi][n][c]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wt = wave & 1, wn = wave >> 1;
 
   const int n_tiles = krrn_cdiv(a.N, kWN);
   const int bid = krrn_xcd_remap(blockIdx.x, krrn_cdiv(a.T, kWT) * n_tiles);
   const int tb = bid / n_tiles, nb = bid % n_tiles;
   const int t0 = tb * kWT, n0 = nb * kWN;
   const int HWt = a.Ht * a.Wt;
-  constexpr unsigned kOOB = 0xFFFFFFF0u;
 
-  // ---- input staging geometry: thread -> (tile, channel pair) -----------------------
-  const int st = tid >> 3;          // tile inside the block
-  const int scp = (tid & 7) * 2;    // channel pair inside the chunk
+  // ---- staging geometry ---------------------------------------------------------------
+  const int st = tid >> 3;  // tile inside the block
+  const int sc = tid & 7;   // channel inside the chunk
   const int b0 = min(t0, a.T - 1) / HWt;
   const float* abase = a.in + (size_t)b0 * a.img + a.in_co;
   const long long a_avail = ((long long)(a.B - b0) * a.img - a.in_co) * 4;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)abase, (short)0, (int)min(a_avail, (long long)kOOB), 0x00020000);
+      (void*)abase, (short)0, (int)min(a_avail, 0x7FFFFFFFLL), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.U, (short)0, (int)min((long long)16 * a.N * a.cin * 4, (long long)kOOB), 0x00020000);
-  unsigned pbase;    // element offset of patch pixel (0, 0) relative to abase (mod 2^32)
-  unsigned pmask;    // bit 4r + c: patch pixel (r, c) inside the image
+      (void*)a.U, (short)0, (int)min((long long)16 * a.N * a.cin * 4, 0x7FFFFFFFLL), 0x00020000);
+  unsigned poff[16];  // byte offset of patch pixel (r, c), channel sc; kWOOB outside the image
   {
     const int t = t0 + st;
     const bool ok = t < a.T;
@@ -86,46 +84,43 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
     const int rr = tt - b * HWt;
     const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
     const int iy0 = 2 * ty - 1, ix0 = 2 * tx - 1;
-    pbase = (unsigned)((long long)(b - b0) * a.img + ((long long)iy0 * a.W + ix0) * a.in_cs);
-    unsigned m = 0;
+    const long long pb = (long long)(b - b0) * a.img + sc;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int iy = iy0 + r, ix = ix0 + c;
-        m |= (ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? (1u << (4 * r + c)) : 0u;
+        const bool in = ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        poff[4 * r + c] = in ? (unsigned)((pb + ((long long)iy * a.W + ix) * a.in_cs) * 4) : kWOOB;
       }
-    pmask = m;
   }
-  const unsigned rowstep = (unsigned)a.W * (unsigned)a.in_cs;
+  unsigned woff[8];  // byte offset of this thread's 8 weight float4s at chunk 0
+  int wc[8];         // their channel
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + 256 * i;  // (xi, n, c4) over 16 x 64 x 2
+    const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
+    wc[i] = 4 * c4;
+    woff[i] = (n0 + n < a.N) ? (unsigned)((((long long)xi * a.N + n0 + n) * a.cin + 4 * c4) * 4) : kWOOB;
+  }
 
-  f32x2 d[16];
+  float d[16];
   f32x4 w[8];
   auto load_chunk = [&](int c0) {
-    const int ch = c0 + scp;
-    const bool ch_ok = ch < a.cin;  // cin is a multiple of 4 and ch even: the pair is whole
+    const unsigned cb = (unsigned)c0 * 4u;
+    const bool ch_ok = c0 + sc < a.cin;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int p = 4 * r + c;
-        const bool ok = ch_ok && ((pmask >> p) & 1u);
-        const unsigned off = ok ? (pbase + r * rowstep + (unsigned)(c * a.in_cs + ch)) * 4u : kOOB;
-        d[p] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rsA, off, 0, 0));
-      }
+    for (int p = 0; p < 16; ++p)
+      d[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, ch_ok ? poff[p] + cb : kWOOB, 0, 0));
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int e = tid + 256 * i;  // (xi, n, c4) over 16 x 32 x 4
-      const int xi = e >> 7, n = (e >> 2) & 31, c4 = e & 3;
-      const int cc = c0 + 4 * c4;
-      const bool ok = (n0 + n < a.N) && (cc < a.cin);
-      const unsigned off = ok ? (unsigned)(((long long)xi * a.N + n0 + n) * a.cin + cc) * 4u : kOOB;
-      w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, off, 0, 0));
+      const bool ok = c0 + wc[i] < a.cin;
+      w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, ok ? woff[i] + cb : kWOOB, 0, 0));
     }
   };
   auto stage_chunk = [&]() {
-    // V = B^T d B on the channel pair
-    f32x2 t[16];
+    // V = B^T d B
+    float t[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
@@ -135,29 +130,27 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const f32x2 v0 = t[u * 4 + 0] - t[u * 4 + 2];
-      const f32x2 v1 = t[u * 4 + 1] + t[u * 4 + 2];
-      const f32x2 v2 = t[u * 4 + 2] - t[u * 4 + 1];
-      const f32x2 v3 = t[u * 4 + 1] - t[u * 4 + 3];
-      *reinterpret_cast<f32x2*>(As + ((u * 4 + 0) * kWT + st) * kWP + scp) = v0;
-      *reinterpret_cast<f32x2*>(As + ((u * 4 + 1) * kWT + st) * kWP + scp) = v1;
-      *reinterpret_cast<f32x2*>(As + ((u * 4 + 2) * kWT + st) * kWP + scp) = v2;
-      *reinterpret_cast<f32x2*>(As + ((u * 4 + 3) * kWT + st) * kWP + scp) = v3;
+      As[((u * 4 + 0) * kWT + st) * kWP + sc] = t[u * 4 + 0] - t[u * 4 + 2];
+      As[((u * 4 + 1) * kWT + st) * kWP + sc] = t[u * 4 + 1] + t[u * 4 + 2];
+      As[((u * 4 + 2) * kWT + st) * kWP + sc] = t[u * 4 + 2] - t[u * 4 + 1];
+      As[((u * 4 + 3) * kWT + st) * kWP + sc] = t[u * 4 + 1] - t[u * 4 + 3];
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int e = tid + 256 * i;
-      const int xi = e >> 7, n = (e >> 2) & 31, c4 = e & 3;
+      const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
       *reinterpret_cast<f32x4*>(Bs + (xi * kWN + n) * kWP + 4 * c4) = w[i];
     }
   };
 
-  f32x4 acc[16];
+  f32x16 acc[4][2];
 #pragma unroll
-  for (int x = 0; x < 16; ++x) acc[x] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fk = (lane >> 4) * 4;
-  const float* Ar = As + (wt * 16 + fr) * kWP + fk;
-  const float* Br = Bs + (wn * 16 + fr) * kWP + fk;
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
+  const int fr = lane & 31, fk = (lane >> 5) * 4;
 
   const int nchunks = krrn_cdiv(a.cin, kWC);
   load_chunk(0);
@@ -166,49 +159,72 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
     __syncthreads();
     if (ck + 1 < nchunks) load_chunk((ck + 1) * kWC);  // in flight during the MFMAs
 #pragma unroll
-    for (int x = 0; x < 16; ++x) {
-      const f32x4 av = *reinterpret_cast<const f32x4*>(Ar + x * kWT * kWP);
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(Br + x * kWN * kWP);
+    for (int x = 0; x < 4; ++x) {
+      const int xi = 4 * wave + x;
+      const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc[x], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
+      }
     }
     __syncthreads();
   }
 
-  // ---- output transform Y = A^T M A + epilogue, lane-local --------------------------------
-  const int n = n0 + wn * 16 + fr;
-  if (n >= a.n_store) return;
-  const float sc = a.scale ? a.scale[n] : 1.f;
-  const float bi = a.bias ? a.bias[n] : 0.f;
+  // ---- output transform Y = A^T M A + epilogue, one 32-channel n-block at a time ------------
+  float* Ms = smem;  // [xi][tile][n] pitch kMP
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int t = t0 + wt * 16 + (lane >> 4) * 4 + r;
-    if (t >= a.T) continue;
-    float s0[4], s1[4];
+  for (int j = 0; j < 2; ++j) {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const float m0 = acc[0 * 4 + v][r], m1 = acc[1 * 4 + v][r], m2 = acc[2 * 4 + v][r], m3 = acc[3 * 4 + v][r];
-      s0[v] = m0 + m1 + m2;
-      s1[v] = m1 - m2 - m3;
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        Ms[((4 * wave + x) * kWT + row) * kMP + fr] = acc[x][j][r];
+      }
+    __syncthreads();
+    const int nl = tid & 31;
+    const int n = n0 + j * 32 + nl;
+    if (n < a.n_store) {
+      const float scl = a.scale ? a.scale[n] : 1.f;
+      const float bi = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int tl = (tid >> 5) + 8 * q4;
+        const int t = t0 + tl;
+        if (t >= a.T) continue;
+        float m[16];
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) m[xi] = Ms[(xi * kWT + tl) * kMP + nl];
+        float s0[4], s1[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          s0[v] = m[0 * 4 + v] + m[1 * 4 + v] + m[2 * 4 + v];
+          s1[v] = m[1 * 4 + v] - m[2 * 4 + v] - m[3 * 4 + v];
+        }
+        float y[4];
+        y[0] = s0[0] + s0[1] + s0[2];
+        y[1] = s0[1] - s0[2] - s0[3];
+        y[2] = s1[0] + s1[1] + s1[2];
+        y[3] = s1[1] - s1[2] - s1[3];
+        const int b = t / HWt;
+        const int rr = t - b * HWt;
+        const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+          if (oy >= a.H || ox >= a.W) continue;
+          const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+          float v = y[q] * scl + bi;
+          if (a.res) v += a.res[pix * a.res_cs + a.res_co + n];
+          if (a.relu) v = fmaxf(v, 0.f);
+          a.out[pix * a.out_cs + a.out_co + n] = v;
+        }
+      }
     }
-    float y[4];
-    y[0] = s0[0] + s0[1] + s0[2];
-    y[1] = s0[1] - s0[2] - s0[3];
-    y[2] = s1[0] + s1[1] + s1[2];
-    y[3] = s1[1] - s1[2] - s1[3];
-    const int b = t / HWt;
-    const int rr = t - b * HWt;
-    const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-      if (oy >= a.H || ox >= a.W) continue;
-      const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
-      float v = y[q] * sc + bi;
-      if (a.res) v += a.res[pix * a.res_cs + a.res_co + n];
-      if (a.relu) v = fmaxf(v, 0.f);
-      a.out[pix * a.out_cs + a.out_co + n] = v;
-    }
+    __syncthreads();
   }
 }
 
@@ -220,8 +236,8 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
                                    int relu, void* stream) {
   if (!in || !U || !out) return KRRN_EARG;
   if (B < 1 || H < 1 || W < 1 || N < 1 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
-  if (cin < 4 || (cin & 3) || (in_cs & 1) || (in_co & 1) || in_co + cin > in_cs) return KRRN_EALIGN;
-  if (!krrn_aligned16(U) || (((uintptr_t)in) & 7u)) return KRRN_EALIGN;
+  if (cin < 4 || (cin & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(U) || (((uintptr_t)in) & 3u)) return KRRN_EALIGN;
   if (out_co + n_store > out_cs) return KRRN_ESHAPE;
   WinoArgs a;
   a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = H; a.W = W; a.cin = cin;
@@ -235,7 +251,7 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   a.T = (int)T;
   // 32-bit buffer offsets: the images one block's 32 tiles touch, and the weights
   const long long span = ((kWT + (long long)a.Ht * a.Wt - 1) / ((long long)a.Ht * a.Wt) + 1) * a.img * 4;
-  if (span >= 0xFFFFFFF0LL || 16LL * N * cin * 4 >= 0xFFFFFFF0LL) return KRRN_ESHAPE;
+  if (span >= 0x7FFF0000LL || 16LL * N * cin * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long blocks = (long long)krrn_cdiv(a.T, kWT) * krrn_cdiv(N, kWN);
   if (blocks > 0x7fffffffLL) return KRRN_ESHAPE;
   hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
