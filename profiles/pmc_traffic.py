@@ -15,9 +15,11 @@ from collections import defaultdict
 
 
 def _short(name: str) -> str:
-    m = re.search(r"conv_gemm_f32_kernel<(\d+), (\d+), (true|false)>", name)
+    m = re.search(r"conv_gemm_f32_kernel<(\d+), (\d+), (\d+), \d+, (true|false)>", name)
     if m:
-        return f"conv_gemm_f32<{m.group(1)},{m.group(2)}>" + (",nchw" if m.group(3) == "true" else "")
+        return f"conv_gemm_f32<{m.group(1)},{m.group(2)},{m.group(3)}>" + (",nchw" if m.group(4) == "true" else "")
+    if "wino_f23_kernel" in name:
+        return "wino_f23<32,32,16>"
     m = re.search(r"(\w+_kernel)", name)
     return m.group(1) if m else name
 
