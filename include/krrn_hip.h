@@ -88,8 +88,9 @@ int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* st
 
 /* 3x3 stride-1 pad-1 convolution by fused Winograd F(2x2, 3x3) (the head / last_layer /
  * deconv-BasicBlock convs: krrn.py:46-84, myhrnet.py:324-346; cuDNN / MIOpen use the same
- * algorithm for these f32 convs). U = G g G^T are the transformed weights, [16][N][cin] f32
- * (element xi = 4u + v of the 4x4 transform), computed once per plan; epilogue as
+ * algorithm for these f32 convs). U = G g G^T are the transformed weights, f32 in chunk-major
+ * order [ceil(cin/8)][16][N][8] (element xi = 4u + v of the 4x4 transform; input channels
+ * padded to a multiple of 8 with zeros), computed once per plan; epilogue as
  * krrn_conv2d_f32: out = act(scale[n] * conv + bias[n] (+ res)). NHWC in/out with channel
  * stride / offset; cin multiple of 4, U 16-byte aligned. */
 int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* U,

@@ -73,8 +73,9 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
   const long long a_avail = ((long long)(a.B - b0) * a.img - a.in_co) * 4;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void*)abase, (short)0, (int)min(a_avail, 0x7FFFFFFFLL), 0x00020000);
+  const int nchunks = krrn_cdiv(a.cin, kWC);
   const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.U, (short)0, (int)min((long long)16 * a.N * a.cin * 4, 0x7FFFFFFFLL), 0x00020000);
+      (void*)a.U, (short)0, (int)min((long long)nchunks * 16 * a.N * kWC * 4, 0x7FFFFFFFLL), 0x00020000);
   unsigned poff[16];  // byte offset of patch pixel (r, c), channel sc; kWOOB outside the image
   {
     const int t = t0 + st;
@@ -94,29 +95,29 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
         poff[4 * r + c] = in ? (unsigned)((pb + ((long long)iy * a.W + ix) * a.in_cs) * 4) : kWOOB;
       }
   }
+  // U is chunk-major [chunk][xi][N][8]: one chunk of one block is 16 contiguous 2 KB runs
   unsigned woff[8];  // byte offset of this thread's 8 weight float4s at chunk 0
-  int wc[8];         // their channel
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int e = tid + 256 * i;  // (xi, n, c4) over 16 x 64 x 2
     const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
-    wc[i] = 4 * c4;
-    woff[i] = (n0 + n < a.N) ? (unsigned)((((long long)xi * a.N + n0 + n) * a.cin + 4 * c4) * 4) : kWOOB;
+    woff[i] = (n0 + n < a.N) ? (unsigned)((((long long)xi * a.N + n0 + n) * kWC + 4 * c4) * 4) : kWOOB;
   }
+  const unsigned wstride = (unsigned)(16 * a.N * kWC * 4);  // bytes per chunk
 
   float d[16];
   f32x4 w[8];
-  auto load_chunk = [&](int c0) {
+  auto load_chunk = [&](int ck) {
+    const int c0 = ck * kWC;
     const unsigned cb = (unsigned)c0 * 4u;
     const bool ch_ok = c0 + sc < a.cin;
 #pragma unroll
     for (int p = 0; p < 16; ++p)
       d[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, ch_ok ? poff[p] + cb : kWOOB, 0, 0));
+    const unsigned wb = (unsigned)ck * wstride;  // padded channels of the last chunk are zero in U
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const bool ok = c0 + wc[i] < a.cin;
-      w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, ok ? woff[i] + cb : kWOOB, 0, 0));
-    }
+    for (int i = 0; i < 8; ++i)
+      w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, woff[i] + wb, 0, 0));
   };
   auto stage_chunk = [&]() {
     // V = B^T d B
@@ -152,12 +153,11 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
       for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
   const int fr = lane & 31, fk = (lane >> 5) * 4;
 
-  const int nchunks = krrn_cdiv(a.cin, kWC);
   load_chunk(0);
   for (int ck = 0; ck < nchunks; ++ck) {
     stage_chunk();
     __syncthreads();
-    if (ck + 1 < nchunks) load_chunk((ck + 1) * kWC);  // in flight during the MFMAs
+    if (ck + 1 < nchunks) load_chunk(ck + 1);  // in flight during the MFMAs
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int xi = 4 * wave + x;
@@ -251,7 +251,7 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   a.T = (int)T;
   // 32-bit buffer offsets: the images one block's 32 tiles touch, and the weights
   const long long span = ((kWT + (long long)a.Ht * a.Wt - 1) / ((long long)a.Ht * a.Wt) + 1) * a.img * 4;
-  if (span >= 0x7FFF0000LL || 16LL * N * cin * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
+  if (span >= 0x7FFF0000LL || (long long)krrn_cdiv(cin, kWC) * 16 * N * kWC * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long blocks = (long long)krrn_cdiv(a.T, kWT) * krrn_cdiv(N, kWN);
   if (blocks > 0x7fffffffLL) return KRRN_ESHAPE;
   hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);

@@ -39,7 +39,11 @@ from .runtime import Late, Plan, add_conv, ptr
 class KRRNPlan:
     """Compiled forward for one (B, S, N, opt_pose)."""
 
-    def __init__(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device):
+    # side stream of the pose step when it is fused into the forward plan (pose_hook)
+    POSE_SID = 6
+
+    def __init__(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device, pose_hook=None,
+                 pose_stream: bool = True):
         self.B, self.S, self.N, self.opt_pose = B, S, N, opt_pose
         cfg = model.cfg
         C = model.num_cls
@@ -93,6 +97,13 @@ class KRRNPlan:
                  ptr(self.cls), ptr(self.xyz), ptr(self.normal), B, Ho, Wo)
         self.specs = [specs, bld.specs]
         self.pred_t = None
+        psid = self.POSE_SID if pose_stream else 0
+        if pose_hook is not None:
+            # get_pose only needs the xyz map and choose (trainer.py:403-412): it runs on its own
+            # stream beside the fusion + TBase chain and joins at the end of the plan
+            plan.fork([psid])
+            with plan.on_stream(psid):
+                pose_hook(self)
         if opt_pose:
             # choose gather (krrn.py:121-122) -> P9 = [cloud | xyz_emb | nml_emb]
             self.p9 = plan.buf((B, N, 9))
@@ -109,6 +120,8 @@ class KRRNPlan:
             self.feat = feat
             self.pred_t, self.tbase_bufs = build_tbase_plan(model.pose.t_net, plan, B, N, feat, "cls", "cloud",
                                                             cfg.Module.POSENet.INC_R, C)
+        if pose_hook is not None:
+            plan.join([psid])
         self.env = {"cls": self.cls, "cloud": self.cloud}
 
     def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):

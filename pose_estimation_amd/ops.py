@@ -208,7 +208,8 @@ WINO_G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0,
 
 def wino_weights(conv: torch.nn.Conv2d, device, cin_map: Optional[List[int]] = None,
                  cin_p: Optional[int] = None) -> torch.Tensor:
-    """[cout, cin, 3, 3] -> U [16][pad4(cout)][cin_p] f32 (xi = 4u + v), transformed in f64."""
+    """[cout, cin, 3, 3] -> U f32 in the kernel's chunk-major order [ceil(cin_p/8)][16][pad4(cout)][8]
+    (xi = 4u + v; channels past cin_p are zero), transformed in f64."""
     w = conv.weight.detach().cpu().double()
     cout, cin = w.shape[:2]
     if cin_map is None:
@@ -217,6 +218,9 @@ def wino_weights(conv: torch.nn.Conv2d, device, cin_map: Optional[List[int]] = N
     u = torch.einsum("ui,ncij,vj->uvnc", WINO_G, w, WINO_G)  # [4, 4, cout, cin]
     out = torch.zeros(16, pad4(cout), cin_p, dtype=torch.float64)
     out[:, :cout, torch.tensor(cin_map, dtype=torch.long)] = u.reshape(16, cout, cin)
+    nck = (cin_p + 7) // 8
+    out = torch.nn.functional.pad(out, (0, 8 * nck - cin_p))
+    out = out.view(16, pad4(cout), nck, 8).permute(2, 0, 1, 3)  # [chunk][xi][n][8]
     return out.float().contiguous().to(device)
 
 

@@ -38,33 +38,41 @@ class _Part:
     inl: torch.Tensor
     lo: int
     hi: int
+    aux: Dict[str, torch.Tensor]  # the device-drawn PnP subset / RANSAC subsets / inlier mask
 
 
 class BatchPipeline:
     def __init__(self, model: KRRN, B: int, S: int, N: int, device, parts: int = 1, seed: int = 0,
-                 inner_streams: bool = True):
+                 inner_streams: bool = True, pose_stream: bool = True):
         if B % parts:
             raise ValueError(f"batch {B} not divisible into {parts} parts")
         self.B, self.S, self.N, self.device = B, S, N, torch.device(device)
         b = B // parts
         self.parts: List[_Part] = []
         for p in range(parts):
-            with torch.no_grad():
-                kp = KRRNPlan(model, b, S, N, True, self.device)
-            kp.seed.fill_(1000003 * (seed + 1) + 7919 * p)
             dev = self.device
             xm = torch.zeros((b, N), device=dev)
             ym = torch.zeros((b, N), device=dev)
             K4 = torch.zeros((b, 4), device=dev)
             ext = torch.zeros((b, 3), dtype=torch.float64, device=dev)
             lfb = torch.zeros((b, 3), dtype=torch.float64, device=dev)
-            pose = Plan(dev)
-            R, t, inl, _ = add_pose_ops(pose, kp.xyz, kp.choose.view(b, N), b, N, xm, ym, K4, ext, lfb, kp.seed)
+            res = {}
+
+            def hook(kp, res=res, xm=xm, ym=ym, K4=K4, ext=ext, lfb=lfb):
+                res["pose"] = add_pose_ops(kp.plan, kp.xyz, kp.choose.view(b, N), b, N, xm, ym, K4, ext, lfb, kp.seed)
+
+            with torch.no_grad():
+                kp = KRRNPlan(model, b, S, N, True, self.device, pose_hook=hook, pose_stream=pose_stream)
+            kp.seed.fill_(1000003 * (seed + 1) + 7919 * p)
+            R, t, inl, aux = res["pose"]
+            pose = Plan(dev)  # after the forward plan: every reader of the seed has run
             pose.add("krrn_rng_advance", ptr(kp.seed))
-            self.parts.append(_Part(kp, pose, xm, ym, K4, ext, lfb, R, t, inl, p * b, (p + 1) * b))
+            self.parts.append(_Part(kp, pose, xm, ym, K4, ext, lfb, R, t, inl, p * b, (p + 1) * b, aux))
         self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)] if parts > 1 else []
         self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.inner_streams = inner_streams
+        # parts > 1 runs each part's plan serially on its part stream: capturing nested plan side
+        # streams under per-part streams segfaults in hipStreamEndCapture (measured on ROCm 7.2)
+        self.inner_streams = inner_streams and parts == 1
 
     # -- inputs / outputs ------------------------------------------------------------------
     def load(self, data: Dict[str, torch.Tensor]):
