@@ -41,9 +41,10 @@ def roofline_from_profile(prof, B: int):
     groups = {}
     for op, ms in prof:
         k = op.meta.get("kernel", op.name)
-        g = groups.setdefault(k, {"ms": 0.0, "flops": 0.0, "n": 0})
+        g = groups.setdefault(k, {"ms": 0.0, "flops": 0.0, "mfma": 0.0, "n": 0})
         g["ms"] += ms
         g["flops"] += op.meta.get("flops", 0.0)
+        g["mfma"] += op.meta.get("mfma_flops", op.meta.get("flops", 0.0))
         g["n"] += 1
     total_ms = sum(g["ms"] for g in groups.values())
     dom = max(groups, key=lambda k: groups[k]["ms"])
@@ -66,6 +67,13 @@ def roofline_from_profile(prof, B: int):
                               "TFLOP/s": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2) if conv_ms else None,
                               "GFLOP_per_crop": round(conv_fl / B / 1e9, 3)},
             "events_ms_per_step": round(total_ms, 3)}
+    if g["mfma"] and abs(g["mfma"] - g["flops"]) > 1e-6 * g["flops"]:
+        # Winograd: `achieved` counts the direct-conv FLOPs the launch replaces (SURVEY §8d's
+        # formula), so frac can exceed 1; this is what the matrix pipe actually issued
+        mp = (g["mfma"] / g["n"]) / (avg_ms * 1e-3) / 1e12
+        roof["mfma_pipe"] = {"achieved": round(mp, 2), "frac": round(mp / PEAK_F32_MFMA_TFLOPS, 4),
+                             "flops_per_launch": round(g["mfma"] / g["n"]),
+                             "note": "F(2x2,3x3) Winograd issues 2.25x fewer MFMA FLOPs than the direct conv"}
     return roof, breakdown
 
 

@@ -26,13 +26,14 @@
 // M goes through LDS once per 32-channel n-block at the end.
 #include "krrn_common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int kWT = 32;       // tiles per block
 constexpr int kWN = 64;       // output channels per block
 constexpr int kWC = 8;        // input channels per chunk
 constexpr int kWP = kWC + 4;  // LDS row pitch (floats): 3 x 16 B
-constexpr int kMP = 33;       // output-staging pitch
 constexpr unsigned kWOOB = 0xFFFF0000u;  // > any valid offset, and + channel offsets stays > it
 
 struct WinoArgs {
@@ -49,35 +50,111 @@ struct WinoArgs {
   float* out;
   int out_cs, out_co;
   int relu;
+  int vec;        // float4 epilogue (16-B aligned channel runs, n_store % 4 == 0)
   int Ht, Wt, T;  // tiles per column / row, total tiles
 };
 
-__global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[16 * (kWT + kWN) * kWP];
-  float* As = smem;                   // [xi][tile][c]
-  float* Bs = smem + 16 * kWT * kWP;  // [xi][n][c]
+// Output transform Y = A^T M A + epilogue. Wave w holds row u = w of the 4x4 component grid
+// (acc[x] = component v = x) for every (tile, channel) of the block, so the column combination
+// c0 = M[u][0]+M[u][1]+M[u][2], c1 = M[u][1]-M[u][2]-M[u][3] is lane-local; only (c0, c1)
+// go through LDS ([u][c][tile][n], pitch kSP), and each thread then finishes the row
+// combination for 2 (tile, 4-channel) pairs and stores 2x2 pixels x float4.
+constexpr int kSP = kWN + 4;
+static_assert(4 * 2 * kWT * kSP <= 16 * (kWT + kWN) * kWP, "epilogue staging must fit the main-loop LDS");
+
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f32x16 (&acc)[4][2], int t0, int n0,
+                                              int HWt) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 31;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const float m0 = acc[0][j][r], m1 = acc[1][j][r], m2 = acc[2][j][r], m3 = acc[3][j][r];
+      smem[((wave * 2 + 0) * kWT + row) * kSP + j * 32 + fr] = m0 + m1 + m2;
+      smem[((wave * 2 + 1) * kWT + row) * kSP + j * 32 + fr] = m1 - m2 - m3;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pr = tid + 256 * i;
+    const int n4 = pr & 15, tl = pr >> 4;
+    const int t = t0 + tl;
+    const int n = n0 + 4 * n4;
+    if (t >= a.T || n >= a.n_store) continue;
+    f32x4 c[4][2];  // [u][c]
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) c[u][q] = *reinterpret_cast<const f32x4*>(smem + ((u * 2 + q) * kWT + tl) * kSP + 4 * n4);
+    f32x4 y[4];
+    y[0] = c[0][0] + c[1][0] + c[2][0];
+    y[1] = c[0][1] + c[1][1] + c[2][1];
+    y[2] = c[1][0] - c[2][0] - c[3][0];
+    y[3] = c[1][1] - c[2][1] - c[3][1];
+    const int b = t / HWt;
+    const int rr = t - b * HWt;
+    const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
+    if (a.vec) {
+      const f32x4 scl = a.scale ? *reinterpret_cast<const f32x4*>(a.scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+      const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+        if (oy >= a.H || ox >= a.W) continue;
+        const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+        f32x4 v = y[q] * scl + bi;
+        if (a.res) v += *reinterpret_cast<const f32x4*>(a.res + pix * a.res_cs + a.res_co + n);
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        *reinterpret_cast<f32x4*>(a.out + pix * a.out_cs + a.out_co + n) = v;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+        if (oy >= a.H || ox >= a.W) continue;
+        const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (n + e >= a.n_store) break;
+          float v = y[q][e] * (a.scale ? a.scale[n + e] : 1.f) + (a.bias ? a.bias[n + e] : 0.f);
+          if (a.res) v += a.res[pix * a.res_cs + a.res_co + n + e];
+          if (a.relu) v = fmaxf(v, 0.f);
+          a.out[pix * a.out_cs + a.out_co + n + e] = v;
+        }
+      }
+    }
+  }
+}
 
-  const int n_tiles = krrn_cdiv(a.N, kWN);
-  const int bid = krrn_xcd_remap(blockIdx.x, krrn_cdiv(a.T, kWT) * n_tiles);
-  const int tb = bid / n_tiles, nb = bid % n_tiles;
-  const int t0 = tb * kWT, n0 = nb * kWN;
-  const int HWt = a.Ht * a.Wt;
-
-  // ---- staging geometry ---------------------------------------------------------------
-  const int st = tid >> 3;  // tile inside the block
-  const int sc = tid & 7;   // channel inside the chunk
-  const int b0 = min(t0, a.T - 1) / HWt;
-  const float* abase = a.in + (size_t)b0 * a.img + a.in_co;
-  const long long a_avail = ((long long)(a.B - b0) * a.img - a.in_co) * 4;
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)abase, (short)0, (int)min(a_avail, 0x7FFFFFFFLL), 0x00020000);
-  const int nchunks = krrn_cdiv(a.cin, kWC);
-  const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.U, (short)0, (int)min((long long)nchunks * 16 * a.N * kWC * 4, 0x7FFFFFFFLL), 0x00020000);
+// Staging of one 8-channel chunk: thread (tile st, channel sc) loads its 4x4 input patch
+// (raw buffer loads; out-of-image pixels and channels past cin return 0 = the conv's zero
+// padding) and 8 float4s of the chunk-major weights; stage() writes V = B^T d B and the
+// weights k-contiguous into LDS.
+struct WinoStager {
+  __amdgpu_buffer_rsrc_t rsA, rsU;
   unsigned poff[16];  // byte offset of patch pixel (r, c), channel sc; kWOOB outside the image
-  {
+  unsigned woff[8];   // byte offset of this thread's 8 weight float4s at chunk 0
+  unsigned wstride;   // bytes per weight chunk
+  int st, sc, cin, nchunks;
+
+  __device__ __forceinline__ WinoStager(const WinoArgs& a, int t0, int n0, int HWt) {
+    const int tid = threadIdx.x;
+    st = tid >> 3;
+    sc = tid & 7;
+    cin = a.cin;
+    nchunks = krrn_cdiv(a.cin, kWC);
+    const int b0 = min(t0, a.T - 1) / HWt;
+    const float* abase = a.in + (size_t)b0 * a.img + a.in_co;
+    const long long a_avail = ((long long)(a.B - b0) * a.img - a.in_co) * 4;
+    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, (int)min(a_avail, 0x7FFFFFFFLL), 0x00020000);
+    rsU = __builtin_amdgcn_make_buffer_rsrc((void*)a.U, (short)0,
+                                            (int)min((long long)nchunks * 16 * a.N * kWC * 4, 0x7FFFFFFFLL), 0x00020000);
     const int t = t0 + st;
     const bool ok = t < a.T;
     const int tt = ok ? t : 0;
@@ -94,32 +171,32 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
         const bool in = ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
         poff[4 * r + c] = in ? (unsigned)((pb + ((long long)iy * a.W + ix) * a.in_cs) * 4) : kWOOB;
       }
-  }
-  // U is chunk-major [chunk][xi][N][8]: one chunk of one block is 16 contiguous 2 KB runs
-  unsigned woff[8];  // byte offset of this thread's 8 weight float4s at chunk 0
+    // U is chunk-major [chunk][xi][N][8]: one chunk of one block is 16 contiguous 2 KB runs
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int e = tid + 256 * i;  // (xi, n, c4) over 16 x 64 x 2
-    const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
-    woff[i] = (n0 + n < a.N) ? (unsigned)((((long long)xi * a.N + n0 + n) * kWC + 4 * c4) * 4) : kWOOB;
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i;  // (xi, n, c4) over 16 x 64 x 2
+      const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
+      woff[i] = (n0 + n < a.N) ? (unsigned)((((long long)xi * a.N + n0 + n) * kWC + 4 * c4) * 4) : kWOOB;
+    }
+    wstride = (unsigned)(16 * a.N * kWC * 4);
   }
-  const unsigned wstride = (unsigned)(16 * a.N * kWC * 4);  // bytes per chunk
 
-  float d[16];
-  f32x4 w[8];
-  auto load_chunk = [&](int ck) {
+  // chunks past the last one load zeros (out-of-range buffer offsets), branch-free
+  __device__ __forceinline__ void load(int ck, float (&d)[16], f32x4 (&w)[8]) const {
     const int c0 = ck * kWC;
     const unsigned cb = (unsigned)c0 * 4u;
-    const bool ch_ok = c0 + sc < a.cin;
+    const unsigned cmask = (c0 + sc < cin) ? 0u : kWOOB;
 #pragma unroll
     for (int p = 0; p < 16; ++p)
-      d[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, ch_ok ? poff[p] + cb : kWOOB, 0, 0));
-    const unsigned wb = (unsigned)ck * wstride;  // padded channels of the last chunk are zero in U
+      d[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, (poff[p] + cb) | cmask, 0, 0));
+    const unsigned wmask = (ck < nchunks) ? 0u : kWOOB;  // padded channels of the last chunk are zero in U
+    const unsigned wb = (unsigned)ck * wstride;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, woff[i] + wb, 0, 0));
-  };
-  auto stage_chunk = [&]() {
+      w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, (woff[i] + wb) | wmask, 0, 0));
+  }
+
+  __device__ __forceinline__ void stage(const float (&d)[16], const f32x4 (&w)[8], float* As, float* Bs) const {
     // V = B^T d B
     float t[16];
 #pragma unroll
@@ -136,14 +213,52 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
       As[((u * 4 + 2) * kWT + st) * kWP + sc] = t[u * 4 + 2] - t[u * 4 + 1];
       As[((u * 4 + 3) * kWT + st) * kWP + sc] = t[u * 4 + 1] - t[u * 4 + 3];
     }
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int e = tid + 256 * i;
       const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
       *reinterpret_cast<f32x4*>(Bs + (xi * kWN + n) * kWP + 4 * c4) = w[i];
     }
-  };
+  }
+};
 
+// Wave w owns components xi = 4w .. 4w+3 over the 32 x 64 block: per chunk 32 MFMAs.
+__device__ __forceinline__ void wino_mma(const float* As, const float* Bs, f32x16 (&acc)[4][2]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 31, fk = (lane >> 5) * 4;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const int xi = 4 * wave + x;
+    const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void wino_block(const WinoArgs& a, int& t0, int& n0, int& HWt) {
+  const int n_tiles = krrn_cdiv(a.N, kWN);
+  const int bid = krrn_xcd_remap(blockIdx.x, krrn_cdiv(a.T, kWT) * n_tiles);
+  const int tb = bid / n_tiles, nb = bid % n_tiles;
+  t0 = tb * kWT;
+  n0 = nb * kWN;
+  HWt = a.Ht * a.Wt;
+}
+
+// v1: single LDS buffer (73.5 KB) -> 2 blocks per CU; one block's staging overlaps the
+// other's MFMAs, the next chunk's global loads are in flight during the current MFMAs.
+__global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[16 * (kWT + kWN) * kWP];
+  float* As = smem;                   // [xi][tile][c]
+  float* Bs = smem + 16 * kWT * kWP;  // [xi][n][c]
+  int t0, n0, HWt;
+  wino_block(a, t0, n0, HWt);
+  const WinoStager sg(a, t0, n0, HWt);
   f32x16 acc[4][2];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
@@ -151,81 +266,51 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
-  const int fr = lane & 31, fk = (lane >> 5) * 4;
-
-  load_chunk(0);
-  for (int ck = 0; ck < nchunks; ++ck) {
-    stage_chunk();
+  float d[16];
+  f32x4 w[8];
+  sg.load(0, d, w);
+  for (int ck = 0; ck < sg.nchunks; ++ck) {
+    sg.stage(d, w, As, Bs);
     __syncthreads();
-    if (ck + 1 < nchunks) load_chunk(ck + 1);  // in flight during the MFMAs
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int xi = 4 * wave + x;
-      const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
-      }
-    }
+    sg.load(ck + 1, d, w);  // in flight during the MFMAs (zeros past the last chunk)
+    wino_mma(As, Bs, acc);
     __syncthreads();
   }
+  wino_epilogue(a, smem, acc, t0, n0, HWt);
+}
 
-  // ---- output transform Y = A^T M A + epilogue, one 32-channel n-block at a time ------------
-  float* Ms = smem;  // [xi][tile][n] pitch kMP
+// v2: double-buffered LDS (2 x 73.5 KB, one block per CU, one wave per SIMD): chunk ck's
+// MFMAs run from one buffer while chunk ck+1 (loaded during the previous chunk) is transformed
+// into the other, then chunk ck+2's loads are issued; one barrier per chunk. The staging
+// instructions sit in the MFMAs' issue shadow of the same wave.
+__global__ __launch_bounds__(256, 1) void wino_f23_db_kernel(const WinoArgs a) {
+  constexpr int kStage = 16 * (kWT + kWN) * kWP;
+  __shared__ __attribute__((aligned(16))) float smem[2 * kStage];
+  int t0, n0, HWt;
+  wino_block(a, t0, n0, HWt);
+  const WinoStager sg(a, t0, n0, HWt);
+  f32x16 acc[4][2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        Ms[((4 * wave + x) * kWT + row) * kMP + fr] = acc[x][j][r];
-      }
-    __syncthreads();
-    const int nl = tid & 31;
-    const int n = n0 + j * 32 + nl;
-    if (n < a.n_store) {
-      const float scl = a.scale ? a.scale[n] : 1.f;
-      const float bi = a.bias ? a.bias[n] : 0.f;
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const int tl = (tid >> 5) + 8 * q4;
-        const int t = t0 + tl;
-        if (t >= a.T) continue;
-        float m[16];
-#pragma unroll
-        for (int xi = 0; xi < 16; ++xi) m[xi] = Ms[(xi * kWT + tl) * kMP + nl];
-        float s0[4], s1[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          s0[v] = m[0 * 4 + v] + m[1 * 4 + v] + m[2 * 4 + v];
-          s1[v] = m[1 * 4 + v] - m[2 * 4 + v] - m[3 * 4 + v];
-        }
-        float y[4];
-        y[0] = s0[0] + s0[1] + s0[2];
-        y[1] = s0[1] - s0[2] - s0[3];
-        y[2] = s1[0] + s1[1] + s1[2];
-        y[3] = s1[1] - s1[2] - s1[3];
-        const int b = t / HWt;
-        const int rr = t - b * HWt;
-        const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-          if (oy >= a.H || ox >= a.W) continue;
-          const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
-          float v = y[q] * scl + bi;
-          if (a.res) v += a.res[pix * a.res_cs + a.res_co + n];
-          if (a.relu) v = fmaxf(v, 0.f);
-          a.out[pix * a.out_cs + a.out_co + n] = v;
-        }
-      }
-    }
+      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
+  float d[16];
+  f32x4 w[8];
+  sg.load(0, d, w);
+  sg.stage(d, w, smem, smem + 16 * kWT * kWP);
+  sg.load(1, d, w);
+  __syncthreads();
+  for (int ck = 0; ck < sg.nchunks; ++ck) {
+    float* cur = smem + (ck & 1) * kStage;
+    float* nxt = smem + ((ck + 1) & 1) * kStage;
+    wino_mma(cur, cur + 16 * kWT * kWP, acc);
+    sg.stage(d, w, nxt, nxt + 16 * kWT * kWP);
+    sg.load(ck + 2, d, w);
     __syncthreads();
   }
+  wino_epilogue(a, smem, acc, t0, n0, HWt);
 }
 
 }  // namespace
@@ -246,6 +331,10 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   a.res = res; a.res_cs = res_cs; a.res_co = res_co;
   a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.relu = relu;
   a.Ht = (H + 1) / 2; a.Wt = (W + 1) / 2;
+  const bool ov = !(out_cs & 3) && !(out_co & 3) && krrn_aligned16(out);
+  const bool rv = !res || (!(res_cs & 3) && !(res_co & 3) && krrn_aligned16(res));
+  const bool sv = (!scale || krrn_aligned16(scale)) && (!bias || krrn_aligned16(bias));
+  a.vec = (ov && rv && sv && !(n_store & 3)) ? 1 : 0;
   const long long T = (long long)B * a.Ht * a.Wt;
   if (T > 0x7fffffffLL) return KRRN_ESHAPE;
   a.T = (int)T;
@@ -254,6 +343,13 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   if (span >= 0x7FFF0000LL || (long long)krrn_cdiv(cin, kWC) * 16 * N * kWC * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long blocks = (long long)krrn_cdiv(a.T, kWT) * krrn_cdiv(N, kWN);
   if (blocks > 0x7fffffffLL) return KRRN_ESHAPE;
-  hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  static const int variant = [] {
+    const char* e = getenv("KRRN_WINO_V");
+    return e ? atoi(e) : 1;
+  }();
+  if (variant == 2)
+    hipLaunchKernelGGL(wino_f23_db_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }
