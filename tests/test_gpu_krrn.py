@@ -52,8 +52,33 @@ def _rel(a, b):
 @pytest.mark.parametrize("B,S,N", [(2, 64, 256), (2, 120, 1000)])
 def test_forward_parity(models, dev, B, S, N):
     m, o = models
+    _check_parity(m, o, dev, B, S, N, make_batch(B, S, N, seed=3))
+
+
+# BASELINE.json configs 3-5 at parity-test sizes: all 13 LineMOD classes (C = 13, S from the
+# test-crop histogram), the ClearGrasp-like C = 5 model (normal branch, 5 classes), and the
+# config-5 stress shape (HRNet-W32, N = 4096 points -> k2 = 10 at level 2, S = 320 crops).
+@pytest.mark.parametrize("bb,C,B,S,N,obj", [("w18", 13, 2, 80, 1000, "all"), ("w18", 5, 1, 256, 1000, "cat"),
+                                            ("w32", 1, 1, 320, 4096, "cat")])
+def test_forward_parity_configs(dev, bb, C, B, S, N, obj):
+    cfg = make_config(num_cls=C, backbone=bb)
+    m = KRRN(cfg=cfg)
+    sd = init_weights(m, 1)
+    m = m.to(dev).eval()
+    o = KRRNOracle(num_cls=C, backbone=bb)
+    o.load_state_dict(sd)
+    o.eval()
+    if obj == "all":
+        from pose_estimation_amd.config import LM_OBJLIST
+        d = make_batch(B, S, N, seed=5, objlist=list(LM_OBJLIST))
+    else:
+        d = make_batch(B, S, N, seed=5)
+        d["cls_id"] = ((torch.arange(B) + 1) % C).view(B, 1)  # a class other than 0 when C > 1
+    _check_parity(m, o, dev, B, S, N, d)
+
+
+def _check_parity(m, o, dev, B, S, N, d):
     torch.set_num_threads(8)
-    d = make_batch(B, S, N, seed=3)
     perms = _draw_perms(N, 11)
     out = m(d["img_croped"].to(dev), d["cloud"].to(dev), d["choose"].to(dev), d["cls_id"].to(dev),
             perms=[p.to(dev) for p in perms])
