@@ -162,7 +162,8 @@ int krrn_gather_rows_f32(const void* idx, int idx64, long long idx_bs, int nrows
                          int src_st, float* dst, long long dst_bs, int dst_st, int width, int B, void* stream);
 
 /* TBase conv4 (first 3 outputs, posenet.py:76-80) + pred_t = mean_N(cloud + t_res) (krrn.py:153).
- * h [B][n][C]; w4 [3][C]; b4 [3]; cloud [B][n][3]; pred_t [B][3]; t_res optional [B][n][3]. */
+ * h [B][n][C]; w4 [3][C]; b4 [3]; cloud [B][n][3]; pred_t [B][3]; t_res optional [B][n][3].
+ * C multiple of 4, h and w4 16-byte aligned (KRRN_EALIGN otherwise). */
 int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const float* w4, const float* b4, const float* cloud,
                         float* pred_t, float* t_res, void* stream);
 
@@ -190,6 +191,28 @@ int krrn_ransac_subsets(const unsigned long long* seed_ptr, unsigned int stream_
 
 /* *seed_ptr += 1 (last node of a replayed step). */
 int krrn_rng_advance(unsigned long long* seed_ptr, void* stream);
+
+/* Eval-time KRRNLoss map terms (lib/network/loss.py:57-65 over loss_utils.py:8-70), SURVEY §8f f1.
+ * NCHW maps of B crops with HW pixels: xyz / xyz_gt [B][3][HW] (l1), nml / nml_gt [B][3][HW]
+ * (1 - cosine, CosineSimilarity eps 1e-6), region [B][R][HW] + region_gt int64 [B][HW] and mask
+ * [B][M][HW] + mask_gt int64 [B][HW] (-log(softmax + 1e-6) at the label). Pixels whose target is
+ * all zero (label 0) are excluded; each term = sum / valid count. Any term may be skipped by
+ * passing NULL maps. out f64 [8]: losses xyz, normal, region, mask, then the four valid counts.
+ * ws: f64 workspace of krrn_map_losses_ws(B, HW) doubles. Deterministic (fixed-order sums). */
+int krrn_map_losses_ws(int B, int HW, long long* n_doubles);
+int krrn_map_losses_f32(const float* xyz, const float* xyz_gt, const float* nml, const float* nml_gt,
+                        const float* region, int R, const long long* region_gt, const float* mask, int M,
+                        const long long* mask_gt, int B, int HW, double* ws, double* out, void* stream);
+
+/* PoseLoss (lib/network/loss.py:19-42) with the GT rotation and the predicted translation as
+ * KRRNLoss calls it (:66-67): pred = model_points [B][P][3] @ target_r[b]^T + pred_t[b]; for
+ * crops whose cls_id is in sym[0..nsym) each predicted point takes its nearest target point
+ * (squared distance, ties -> lower index; the KeOps argkmin of train.py:126); out f64 [1] =
+ * mean over crops of mean_P |pred - target|. ws: krrn_pose_loss_ws(B, P) doubles. */
+int krrn_pose_loss_ws(int B, int P, long long* n_doubles);
+int krrn_pose_loss_f32(const float* target_r, const float* pred_t, const float* target, const float* model_points,
+                       const long long* cls_id, const int* sym, int nsym, int B, int P, double* ws, double* out,
+                       void* stream);
 
 #ifdef __cplusplus
 }

@@ -7,9 +7,11 @@ Drop-in API (the reference's names):
     get_pose(pred, data)                  tools/trainer.py:383-438 (Trainer.get_pose)
     PoseDataset / make_batch              dataset/linemod/batchdataset.py (synthetic frames)
     Metric                                lib/utils/metric.py
+    KRRNLoss                              lib/network/loss.py (eval-time terms)
 """
 from .config import CONFIG, Cfg, make_config  # noqa: F401
 from .krrn import KRRN  # noqa: F401
+from .loss import KRRNLoss  # noqa: F401
 from .pose import get_pose  # noqa: F401
 
-__all__ = ["KRRN", "get_pose", "make_config", "CONFIG", "Cfg"]
+__all__ = ["KRRN", "KRRNLoss", "get_pose", "make_config", "CONFIG", "Cfg"]

@@ -74,6 +74,10 @@ def make_config(num_cls: int = 1, backbone: str = "w18", num_points: int = 1000,
             "POSENet": {"INC_R": 1280, "OUT_T": 3, "OUTC_R": 4},
         },
         "Data": {"NUM_POINTS": num_points, "RESIZE": False},
+        # KRRNLoss weights (lib/network/loss.py:56, cfg.Train.Loss.LOSS_WEIGHT): the values are in
+        # the empty config file too, so every term is weighted 1 unless overridden
+        "Train": {"Loss": {"LOSS_WEIGHT": {"weight_xyz": 1.0, "weight_region": 1.0, "weight_mask": 1.0,
+                                           "weight_normal": 1.0, "weight_pose": 1.0}}},
     })
     for k, v in overrides.items():
         node = cfg

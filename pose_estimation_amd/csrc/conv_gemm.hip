@@ -503,6 +503,8 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
   if (st != KRRN_OK) return st;
   hipStream_t s = (hipStream_t)stream;
   if (out_nchw) {
+    // narrow heads (mask/region/xyz logits, 3C normals): 32-wide N tiles waste least MFMA work
+    if (tile == 6) return launch<128, 32, 32, 4, true>(a, 1, s);
     if (tile == 1 || tile == 4) return launch<128, 128, 16, 2, true>(a, 1, s);
     if (tile == 2 || tile == 7) return launch<128, 64, 16, 2, true>(a, 1, s);
     return launch<64, 64, 16, 2, true>(a, 1, s);

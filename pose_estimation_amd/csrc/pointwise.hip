@@ -31,14 +31,17 @@ __device__ __forceinline__ void src_index(int dst, int in_size, float scale, int
   l0 = 1.f - lam;
 }
 
+// IT = the flat-index type: 32-bit whenever the launch fits (64-bit division is emulated and
+// dominated these memory-bound kernels)
+template <typename IT>
 __global__ void resize_bilinear_kernel(const float* __restrict__ in, int Hi, int Wi, int in_cs, int in_co, int C4,
                                        float* __restrict__ out, int Ho, int Wo, int out_cs, int out_co,
                                        const float* __restrict__ add, int add_cs, int add_co, float sh, float sw,
-                                       int align, int relu, long long total) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                                       int align, int relu, IT total) {
+  const IT e = (IT)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int c4 = (int)(e % C4);
-  long long p = e / C4;
+  IT p = e / C4;
   const int ox = (int)(p % Wo);
   p /= Wo;
   const int oy = (int)(p % Ho);
@@ -61,10 +64,11 @@ __global__ void resize_bilinear_kernel(const float* __restrict__ in, int Hi, int
   *reinterpret_cast<f32x4*>(out + opix * out_cs + out_co + 4 * c4) = r;
 }
 
+template <typename IT>
 __global__ void add_relu_kernel(const float* __restrict__ a, int a_cs, int a_co, const float* __restrict__ b,
                                 int b_cs, int b_co, float* __restrict__ out, int o_cs, int o_co, int C4, int relu,
-                                long long total) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                                IT total) {
+  const IT e = (IT)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int c4 = (int)(e % C4);
   const long long pix = e / C4;
@@ -156,6 +160,10 @@ __global__ void gather_rows_kernel(const void* __restrict__ idx, long long idx_b
 }
 
 // pred_t[b] = mean_i( cloud[b, i] + W4[0:3] . h[b, i] + b4[0:3] )   (one block per crop)
+// TBase conv4 (C -> 3, +bias) and pred_t = mean_N(cloud + t_res) (posenet.py:80, krrn.py:150-153).
+// One block per crop; 4 lanes per point, each lane a float4 stripe of the C-channel row (a wave
+// reads 16 rows x 64 contiguous bytes per load), 2 shuffles finish the dot product. The mean is a
+// fixed-order reduction (per-lane partials, then a fixed tree), so runs are bit-reproducible.
 __global__ __launch_bounds__(256) void tbase_tail_kernel(const float* __restrict__ h, int n, int C,
                                                          const float* __restrict__ w4,
                                                          const float* __restrict__ b4,
@@ -164,33 +172,48 @@ __global__ __launch_bounds__(256) void tbase_tail_kernel(const float* __restrict
   __shared__ float red[4][3];
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane & 3, pl = lane >> 2;
+  const int C4 = C >> 2;
+  const float bx = b4[0], by = b4[1], bz = b4[2];
   float sx = 0.f, sy = 0.f, sz = 0.f;
-  for (int i = wave; i < n; i += 4) {
-    const float* hr = h + ((long long)b * n + i) * C;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float x = hr[c];
-      a0 += w4[c] * x;
-      a1 += w4[C + c] * x;
-      a2 += w4[2 * C + c] * x;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      a0 += __shfl_xor(a0, off);
-      a1 += __shfl_xor(a1, off);
-      a2 += __shfl_xor(a2, off);
-    }
-    const float t0 = a0 + b4[0], t1 = a1 + b4[1], t2 = a2 + b4[2];
-    const float* cp = cloud + ((long long)b * n + i) * 3;
-    if (lane == 0) {
-      if (t_res) {
-        float* tr = t_res + ((long long)b * n + i) * 3;
-        tr[0] = t0; tr[1] = t1; tr[2] = t2;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + wave * 16 + pl;
+    if (i < n) {
+      const f32x4* hr = reinterpret_cast<const f32x4*>(h + ((long long)b * n + i) * C);
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      for (int c4 = q; c4 < C4; c4 += 4) {
+        const f32x4 x = hr[c4];
+        const f32x4 w0 = reinterpret_cast<const f32x4*>(w4)[c4];
+        const f32x4 w1 = reinterpret_cast<const f32x4*>(w4 + C)[c4];
+        const f32x4 w2 = reinterpret_cast<const f32x4*>(w4 + 2 * C)[c4];
+        a0 += w0[0] * x[0] + w0[1] * x[1] + w0[2] * x[2] + w0[3] * x[3];
+        a1 += w1[0] * x[0] + w1[1] * x[1] + w1[2] * x[2] + w1[3] * x[3];
+        a2 += w2[0] * x[0] + w2[1] * x[1] + w2[2] * x[2] + w2[3] * x[3];
       }
-      sx += cp[0] + t0;
-      sy += cp[1] + t1;
-      sz += cp[2] + t2;
+      a0 += __shfl_xor(a0, 1);
+      a1 += __shfl_xor(a1, 1);
+      a2 += __shfl_xor(a2, 1);
+      a0 += __shfl_xor(a0, 2);
+      a1 += __shfl_xor(a1, 2);
+      a2 += __shfl_xor(a2, 2);
+      if (q == 0) {
+        const float t0 = a0 + bx, t1 = a1 + by, t2 = a2 + bz;
+        if (t_res) {
+          float* tr = t_res + ((long long)b * n + i) * 3;
+          tr[0] = t0; tr[1] = t1; tr[2] = t2;
+        }
+        const float* cp = cloud + ((long long)b * n + i) * 3;
+        sx += cp[0] + t0;
+        sy += cp[1] + t1;
+        sz += cp[2] + t2;
+      }
     }
+  }
+#pragma unroll
+  for (int off = 4; off < 64; off <<= 1) {
+    sx += __shfl_xor(sx, off);
+    sy += __shfl_xor(sy, off);
+    sz += __shfl_xor(sz, off);
   }
   if (lane == 0) {
     red[wave][0] = sx; red[wave][1] = sy; red[wave][2] = sz;
@@ -224,9 +247,14 @@ KRRN_API int krrn_resize_bilinear_f32(const float* in, int B, int Hi, int Wi, in
     sw = (float)Wi / (float)Wo;
   }
   const long long total = (long long)B * Ho * Wo * (C / 4);
-  hipLaunchKernelGGL(resize_bilinear_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, in, Hi, Wi, in_cs,
-                     in_co, C / 4, out, Ho, Wo, out_cs, out_co, add, add_cs, add_co, sh, sw, align_corners, relu,
-                     total);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(resize_bilinear_kernel<int>, grid1(total), dim3(256), 0, (hipStream_t)stream, in, Hi, Wi,
+                       in_cs, in_co, C / 4, out, Ho, Wo, out_cs, out_co, add, add_cs, add_co, sh, sw, align_corners,
+                       relu, (int)total);
+  else
+    hipLaunchKernelGGL(resize_bilinear_kernel<long long>, grid1(total), dim3(256), 0, (hipStream_t)stream, in, Hi,
+                       Wi, in_cs, in_co, C / 4, out, Ho, Wo, out_cs, out_co, add, add_cs, add_co, sh, sw,
+                       align_corners, relu, total);
   return krrn_launch_status();
 }
 
@@ -237,8 +265,12 @@ KRRN_API int krrn_add_relu_f32(const float* a, int a_cs, int a_co, const float* 
   if ((C & 3) || (a_cs & 3) || (a_co & 3) || (o_cs & 3) || (o_co & 3) || (b && ((b_cs & 3) || (b_co & 3))))
     return KRRN_EALIGN;
   const long long total = npix * (C / 4);
-  hipLaunchKernelGGL(add_relu_kernel, grid1(total), dim3(256), 0, (hipStream_t)stream, a, a_cs, a_co, b, b_cs, b_co,
-                     out, o_cs, o_co, C / 4, relu, total);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(add_relu_kernel<int>, grid1(total), dim3(256), 0, (hipStream_t)stream, a, a_cs, a_co, b, b_cs,
+                       b_co, out, o_cs, o_co, C / 4, relu, (int)total);
+  else
+    hipLaunchKernelGGL(add_relu_kernel<long long>, grid1(total), dim3(256), 0, (hipStream_t)stream, a, a_cs, a_co, b,
+                       b_cs, b_co, out, o_cs, o_co, C / 4, relu, total);
   return krrn_launch_status();
 }
 
@@ -298,6 +330,7 @@ KRRN_API int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const floa
                                  const float* cloud, float* pred_t, float* t_res, void* stream) {
   if (!h || !w4 || !b4 || !cloud || !pred_t) return KRRN_EARG;
   if (B < 1 || n < 1 || C < 1) return KRRN_ESHAPE;
+  if ((C & 3) || !krrn_aligned16(h) || !krrn_aligned16(w4)) return KRRN_EALIGN;
   hipLaunchKernelGGL(tbase_tail_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, h, n, C, w4, b4, cloud, pred_t,
                      t_res);
   return krrn_launch_status();

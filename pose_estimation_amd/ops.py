@@ -124,6 +124,9 @@ def conv2d_nchw(x: Act, spec: ConvSpec, out: torch.Tensor, n_store: int, relu: b
     B, C, Ho, Wo = out.shape
     np_ = pad4(spec.cout)
     taps = spec.taps[0]
+    if not tile:
+        from .runtime import conv_tile
+        tile = conv_tile(B * Ho * Wo, np_, spec.cin_p, nchw=True)
     _lib.call("krrn_conv2d_f32",
               _ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p,
               Ho, Wo, spec.stride, len(taps), _int_array([t[0] for t in taps]), _int_array([t[1] for t in taps]),

@@ -210,9 +210,10 @@ def conv_tile(M: int, N: int, K: int = 1024, nchw: bool = False) -> int:
     graph-replayed, buffer-load staging): 64x64x32 (4-5 waves/SIMD) is best or within 3% on
     every wide layer (S=120 head conv 119 TF vs 121 for hipBLASLt's f32 GEMM of the same
     shape; TBase conv1 118 TF); 128x32x32 with 4 waves along M for N <= 32 (HRNet branch 0 and
-    its transitions: 51 vs 33 TF). NCHW-output heads use 64x64x16."""
+    its transitions: 51 vs 33 TF). NCHW-output heads use 128x32x32 up to N = 96 (the head
+    logits: N = 72 pads to 3 x 32 instead of 2 x 64), 64x64x16 above."""
     if nchw:
-        return 3
+        return 6 if N <= 96 else 3
     if N <= 32:
         return 6
     return 8

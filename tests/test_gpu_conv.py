@@ -108,18 +108,19 @@ def test_convT(dev, cin, cout, k, p, op, H):
     torch.testing.assert_close(got, ref, **TOL)
 
 
-def test_conv_nchw_out(dev):
+@pytest.mark.parametrize("cout", [70, 3, 130])
+def test_conv_nchw_out(dev, cout):
     g = torch.Generator().manual_seed(5)
-    conv = nn.Conv2d(128, 70, 1, 1, 0, bias=True)
+    conv = nn.Conv2d(128, cout, 1, 1, 0, bias=True)
     with torch.no_grad():
         conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
-        conv.bias.copy_(0.1 * torch.randn(70, generator=g))
+        conv.bias.copy_(0.1 * torch.randn(cout, generator=g))
     x = torch.randn(2, 128, 37, 37, generator=g)
     ref = conv(x).detach()
     spec = ops.make_conv(conv, None, dev)
     xa = _nhwc(x, dev)
-    out = torch.empty(2, 70, 37, 37, device=dev)
-    ops.conv2d_nchw(xa, spec, out, n_store=70)
+    out = torch.empty(2, cout, 37, 37, device=dev)
+    ops.conv2d_nchw(xa, spec, out, n_store=cout)
     torch.cuda.synchronize()
     torch.testing.assert_close(out.cpu(), ref, **TOL)
 
