@@ -214,6 +214,29 @@ int krrn_pose_loss_f32(const float* target_r, const float* pred_t, const float* 
                        const long long* cls_id, const int* sym, int nsym, int B, int P, double* ws, double* out,
                        void* stream);
 
+/* On-GPU input construction, replacing PoseDataset._load_data's per-sample numpy
+ * work (dataset/linemod/batchdataset.py:603-771) for B crops of one snapped square size S.
+ * Frames: rgb u8 [F][H][W][3], depth f32 [F][H][W], mask_label u8 [F][H][W], optional obj_mask u8
+ * [F][H][W] (the reference's mask_obj from the GT coordinate map, :662; NULL = all ones); crop b
+ * reads frame frame[b] at rows rc[2b] .. +S, cols rc[2b+1] .. +S.
+ * krrn_crop_inputs_u8: img f32 [B][3][S][S] = (float(u8 / 255.) - mean) / std (ImageNet, :70, 722,
+ * 744); mask u8 [B][S*S] = mask_label != 0 && depth != 0 (&& obj_mask != 0) (:662-666). */
+int krrn_crop_inputs_u8(const unsigned char* rgb, const float* depth, const unsigned char* mask_label,
+                        const unsigned char* obj_mask, int F, int H, int W, const int* frame, const int* rc, int B,
+                        int S, float* img, unsigned char* mask, void* stream);
+
+/* choose (:667-679): the crop's mask pixels in row-major order; more than N -> a uniformly random
+ * order-preserving N-subset (the N smallest of counter-hash keys of (seed, stream_id, crop, rank),
+ * radix-selected; the reference draws it with np.random.shuffle), fewer -> wrap-padded to N.
+ * Then x_map / y_map = full-frame column / row (:712-715) and cloud [B][N][3] = ((x - cx) * z / fx,
+ * (y - cy) * z / fy, z) with z = depth / depth_scale, f32 arithmetic in the reference's order
+ * (:718-721); K4 [B][4] = fx, fy, cx, cy. count [B] = mask pixels (0 -> zeros everywhere: the
+ * reference drops such a sample). choose int64 [B][N] (crop-local r*S + c). */
+int krrn_choose_points(const unsigned char* mask, int B, int S, int N, const float* depth, int H, int W,
+                       const int* frame, const int* rc, const float* K4, float depth_scale, const long long* seed,
+                       int stream_id, long long* choose, float* cloud, float* xmap, float* ymap, int* count,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif
