@@ -110,6 +110,6 @@ def cal_dis(metric: Metric, pred_r: torch.Tensor, pred_t: torch.Tensor, datas, b
     R = pred_r[b].to(dev).float()
     pts = mp @ R.t() + pred_t[b].reshape(1, 3).to(dev)
     add, _ = metric.cal_adds_cuda(pts, target, int(datas["cls_id"][b]))
-    r = float(metric.angular_distance(R.cpu().reshape(1, 3, 3), datas["target_r"][b].reshape(1, 3, 3)).squeeze())
-    t = float(metric.translation_distance(pred_t[b].cpu().reshape(3), datas["target_t"][b].reshape(3)))
+    r = float(metric.angular_distance(R.cpu().reshape(1, 3, 3), datas["target_r"][b].cpu().reshape(1, 3, 3)).squeeze())
+    t = float(metric.translation_distance(pred_t[b].cpu().reshape(3), datas["target_t"][b].cpu().reshape(3)))
     return add, r, t
