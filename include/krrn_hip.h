@@ -237,6 +237,12 @@ int krrn_choose_points(const unsigned char* mask, int B, int S, int N, const flo
                        int stream_id, long long* choose, float* cloud, float* xmap, float* ymap, int* count,
                        void* stream);
 
+/* Farthest point sampling (tools/script/sample_model.py:35-48): per set b of
+ * pts [B][n][3], out_idx int32 [B][n_samples] = start at 0, then repeatedly the argmax (lowest
+ * index on ties) of the running min distance to the selected set; distances as numpy computes
+ * them (f32, sqrt(((dx*dx + dy*dy) + dz*dz)), no FMA). n <= 16384. */
+int krrn_fps_f32(const float* pts, int B, int n, int n_samples, int* out_idx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

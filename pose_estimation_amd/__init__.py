@@ -8,9 +8,13 @@ Drop-in API (the reference's names):
     PoseDataset / make_batch              dataset/linemod/batchdataset.py (synthetic frames)
     Metric                                lib/utils/metric.py
     KRRNLoss                              lib/network/loss.py (eval-time terms)
+    dataset.PoseDataset / BucketBatcher   dataset/linemod/batchdataset.py + trainer.py:521-551
+    evaluate.test_epoch                   tools/trainer.py:145-250 (batched)
+    fps.farthest_point_sampling           tools/script/sample_model.py:35-48
 """
 from .config import CONFIG, Cfg, make_config  # noqa: F401
 from .krrn import KRRN  # noqa: F401
+from . import dataset, fps  # noqa: F401  (register their C-ABI signatures)
 from .loss import KRRNLoss  # noqa: F401
 from .pose import get_pose  # noqa: F401
 
