@@ -22,11 +22,13 @@
 // k-contiguous in LDS (pitch 12 floats = 3 x 16 B: conflict-free ds_read_b128) so one
 // ds_read_b128 per operand feeds 4 MFMAs. 73.5 KB of LDS -> 2 blocks per CU, so one block's
 // staging overlaps the other's MFMAs; the next chunk's global loads are in flight during the
-// current chunk's MFMAs. The output transform needs all 16 components of a (tile, channel):
-// M goes through LDS once per 32-channel n-block at the end.
+// current chunk's MFMAs. The output transform: wave w holds row u = w of every (tile, channel)'s
+// 4x4 M, so the column combination is lane-local and only 2 of 4 values per row go through LDS;
+// stores are float4 channel runs.
+// Measured and rejected (MI355X, 64 x 128 x 120 x 120): double-buffered LDS at one wave per SIMD
+// (2.24 ms vs 1.50), persistent blocks prefetching the next tile during the epilogue (1.57 ms,
+// register spills), s_setprio around the MFMA cluster (+2 %).
 #include "krrn_common.h"
-
-#include <stdlib.h>
 
 namespace {
 
@@ -62,8 +64,7 @@ struct WinoArgs {
 constexpr int kSP = kWN + 4;
 static_assert(4 * 2 * kWT * kSP <= 16 * (kWT + kWN) * kWP, "epilogue staging must fit the main-loop LDS");
 
-__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f32x16 (&acc)[4][2], int t0, int n0,
-                                              int HWt) {
+__device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][2]) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 31;
@@ -77,13 +78,44 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f3
       smem[((wave * 2 + 1) * kWT + row) * kSP + j * 32 + fr] = m1 - m2 - m3;
     }
   __syncthreads();
+}
+
+__device__ __forceinline__ void wino_epi_finish(const WinoArgs& a, const float* smem, int t0, int n0, int HWt) {
+  const int tid = threadIdx.x;
+  // geometry of this thread's 2 (tile, 4-channel) pairs and their scale / bias
+  int pt[2], pn[2];
+  size_t ppix[2][4];
+  bool pok[2], qok[2][4];
+  f32x4 scl[2], bia[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int pr = tid + 256 * i;
     const int n4 = pr & 15, tl = pr >> 4;
+    pt[i] = tl;
+    pn[i] = n0 + 4 * n4;
     const int t = t0 + tl;
-    const int n = n0 + 4 * n4;
-    if (t >= a.T || n >= a.n_store) continue;
+    pok[i] = t < a.T && pn[i] < a.n_store;
+    const int tt = pok[i] ? t : 0;
+    const int b = tt / HWt;
+    const int rr = tt - b * HWt;
+    const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+      qok[i][q] = pok[i] && oy < a.H && ox < a.W;
+      ppix[i][q] = ((size_t)b * a.H + oy) * a.W + ox;
+    }
+    if (a.vec && pok[i]) {
+      const int n = pn[i];
+      scl[i] = a.scale ? *reinterpret_cast<const f32x4*>(a.scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+      bia[i] = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (!pok[i]) continue;
+    const int tl = pt[i], n = pn[i];
+    const int n4 = (n - n0) >> 2;
     f32x4 c[4][2];  // [u][c]
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -94,31 +126,23 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f3
     y[1] = c[0][1] + c[1][1] + c[2][1];
     y[2] = c[1][0] - c[2][0] - c[3][0];
     y[3] = c[1][1] - c[2][1] - c[3][1];
-    const int b = t / HWt;
-    const int rr = t - b * HWt;
-    const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
     if (a.vec) {
-      const f32x4 scl = a.scale ? *reinterpret_cast<const f32x4*>(a.scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
-      const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-        if (oy >= a.H || ox >= a.W) continue;
-        const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
-        f32x4 v = y[q] * scl + bi;
-        if (a.res) v += *reinterpret_cast<const f32x4*>(a.res + pix * a.res_cs + a.res_co + n);
+        if (!qok[i][q]) continue;
+        f32x4 v = y[q] * scl[i] + bia[i];
+        if (a.res) v += *reinterpret_cast<const f32x4*>(a.res + ppix[i][q] * a.res_cs + a.res_co + n);
         if (a.relu) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        *reinterpret_cast<f32x4*>(a.out + pix * a.out_cs + a.out_co + n) = v;
+        *reinterpret_cast<f32x4*>(a.out + ppix[i][q] * a.out_cs + a.out_co + n) = v;
       }
     } else {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-        if (oy >= a.H || ox >= a.W) continue;
-        const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+        if (!qok[i][q]) continue;
+        const size_t pix = ppix[i][q];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (n + e >= a.n_store) break;
@@ -130,6 +154,12 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f3
       }
     }
   }
+}
+
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f32x16 (&acc)[4][2], int t0, int n0,
+                                              int HWt) {
+  wino_epi_stage(smem, acc);
+  wino_epi_finish(a, smem, t0, n0, HWt);
 }
 
 // Staging of one 8-channel chunk: thread (tile st, channel sc) loads its 4x4 input patch
@@ -250,7 +280,7 @@ __device__ __forceinline__ void wino_block(const WinoArgs& a, int& t0, int& n0, 
   HWt = a.Ht * a.Wt;
 }
 
-// v1: single LDS buffer (73.5 KB) -> 2 blocks per CU; one block's staging overlaps the
+// Single LDS buffer (73.5 KB) -> 2 blocks per CU; one block's staging overlaps the
 // other's MFMAs, the next chunk's global loads are in flight during the current MFMAs.
 __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[16 * (kWT + kWN) * kWP];
@@ -274,40 +304,6 @@ __global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
     __syncthreads();
     sg.load(ck + 1, d, w);  // in flight during the MFMAs (zeros past the last chunk)
     wino_mma(As, Bs, acc);
-    __syncthreads();
-  }
-  wino_epilogue(a, smem, acc, t0, n0, HWt);
-}
-
-// v2: double-buffered LDS (2 x 73.5 KB, one block per CU, one wave per SIMD): chunk ck's
-// MFMAs run from one buffer while chunk ck+1 (loaded during the previous chunk) is transformed
-// into the other, then chunk ck+2's loads are issued; one barrier per chunk. The staging
-// instructions sit in the MFMAs' issue shadow of the same wave.
-__global__ __launch_bounds__(256, 1) void wino_f23_db_kernel(const WinoArgs a) {
-  constexpr int kStage = 16 * (kWT + kWN) * kWP;
-  __shared__ __attribute__((aligned(16))) float smem[2 * kStage];
-  int t0, n0, HWt;
-  wino_block(a, t0, n0, HWt);
-  const WinoStager sg(a, t0, n0, HWt);
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int x = 0; x < 4; ++x)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
-  float d[16];
-  f32x4 w[8];
-  sg.load(0, d, w);
-  sg.stage(d, w, smem, smem + 16 * kWT * kWP);
-  sg.load(1, d, w);
-  __syncthreads();
-  for (int ck = 0; ck < sg.nchunks; ++ck) {
-    float* cur = smem + (ck & 1) * kStage;
-    float* nxt = smem + ((ck + 1) & 1) * kStage;
-    wino_mma(cur, cur + 16 * kWT * kWP, acc);
-    sg.stage(d, w, nxt, nxt + 16 * kWT * kWP);
-    sg.load(ck + 2, d, w);
     __syncthreads();
   }
   wino_epilogue(a, smem, acc, t0, n0, HWt);
@@ -343,13 +339,6 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   if (span >= 0x7FFF0000LL || (long long)krrn_cdiv(cin, kWC) * 16 * N * kWC * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long blocks = (long long)krrn_cdiv(a.T, kWT) * krrn_cdiv(N, kWN);
   if (blocks > 0x7fffffffLL) return KRRN_ESHAPE;
-  static const int variant = [] {
-    const char* e = getenv("KRRN_WINO_V");
-    return e ? atoi(e) : 1;
-  }();
-  if (variant == 2)
-    hipLaunchKernelGGL(wino_f23_db_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }
