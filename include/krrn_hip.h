@@ -161,6 +161,15 @@ int krrn_points_gather_f32(const float* cloud, const float* xyz, const float* nm
 int krrn_gather_rows_f32(const void* idx, int idx64, long long idx_bs, int nrows, const float* src, long long src_bs,
                          int src_st, float* dst, long long dst_bs, int dst_st, int width, int B, void* stream);
 
+/* TBase conv1 over the fusion concat by linearity (krrn.py:132-141 with fusion.py:234-238):
+ * out[b][i] = act(scale * (A[b][ia[b][i]] + B[b][ib[b][i]]) + bias + bias2[b]) over C channels,
+ * with A = fm_5 W1[:, 0:512]^T (level-2 rows, ia = nearest_pool_2) and B = feat_1 W1[:, 512:896]^T +
+ * feat_2 W1[:, 896:1280]^T (level-1 rows, ib = nearest_pool_1); ia / ib int32 [B][n]; bias2
+ * [B][C] optional (the one-hot class column, pre-scaled). C, strides multiple of 4, 16-B aligned. */
+int krrn_gather2_add_f32(const int* ia, const float* A, long long a_bs, int a_st, const int* ib, const float* B_,
+                         long long b_bs, int b_st, int n, int C, const float* scale, const float* bias,
+                         const float* bias2, int relu, float* out, long long o_bs, int o_st, int B, void* stream);
+
 /* TBase conv4 (first 3 outputs, posenet.py:76-80) + pred_t = mean_N(cloud + t_res) (krrn.py:153).
  * h [B][n][C]; w4 [3][C]; b4 [3]; cloud [B][n][3]; pred_t [B][3]; t_res optional [B][n][3].
  * C multiple of 4, h and w4 16-byte aligned (KRRN_EALIGN otherwise). */

@@ -225,6 +225,35 @@ __global__ __launch_bounds__(256) void tbase_tail_kernel(const float* __restrict
   }
 }
 
+// TBase conv1 on the gathered concat, split by linearity (krrn.py:132-141, fusion.py:234-238):
+// feat[i] = [fm_5[nn2[i]] | feat_1[nn1[i]] | feat_2[nn1[i]]], so W1 . feat[i] =
+// P2[nn2[i]] + P1[nn1[i]] with P2 = fm_5 W_a^T on the N/16 level-2 rows and P1 = [feat_1 | feat_2]
+// W_bc^T on the N/4 level-1 rows (5.7x fewer MFMA flops than the GEMM over all N points). This
+// kernel gathers and adds the two row sets and applies the folded BN, the one-hot column
+// (bias2, per crop) and the ReLU: out = act(scale * (A[ia] + B[ib]) + bias + bias2[b]).
+template <typename IT>
+__global__ void gather2_add_kernel(const int* __restrict__ ia, const float* __restrict__ A, long long a_bs, int a_st,
+                                   const int* __restrict__ ib, const float* __restrict__ Bm, long long b_bs,
+                                   int b_st, int n, int C4, const float* __restrict__ scale,
+                                   const float* __restrict__ bias, const float* __restrict__ bias2, int relu,
+                                   float* __restrict__ out, long long o_bs, int o_st, IT total) {
+  const IT e = (IT)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c4 = (int)(e % C4);
+  const IT bi = e / C4;
+  const int i = (int)(bi % n);
+  const int b = (int)(bi / n);
+  const int ra = ia[(long long)b * n + i], rb = ib[(long long)b * n + i];
+  const f32x4 x = *reinterpret_cast<const f32x4*>(A + b * a_bs + (long long)ra * a_st + 4 * c4) +
+                  *reinterpret_cast<const f32x4*>(Bm + b * b_bs + (long long)rb * b_st + 4 * c4);
+  f32x4 v = x * *reinterpret_cast<const f32x4*>(scale + 4 * c4) + *reinterpret_cast<const f32x4*>(bias + 4 * c4);
+  if (bias2) v += *reinterpret_cast<const f32x4*>(bias2 + (long long)b * 4 * C4 + 4 * c4);
+  if (relu) {
+    v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+  }
+  *reinterpret_cast<f32x4*>(out + b * o_bs + (long long)i * o_st + 4 * c4) = v;
+}
+
 inline dim3 grid1(long long total) { return dim3((unsigned)((total + 255) / 256)); }
 
 }  // namespace
@@ -333,5 +362,25 @@ KRRN_API int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const floa
   if ((C & 3) || !krrn_aligned16(h) || !krrn_aligned16(w4)) return KRRN_EALIGN;
   hipLaunchKernelGGL(tbase_tail_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, h, n, C, w4, b4, cloud, pred_t,
                      t_res);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_gather2_add_f32(const int* ia, const float* A, long long a_bs, int a_st, const int* ib, const float* B_,
+                                  long long b_bs, int b_st, int n, int C, const float* scale, const float* bias,
+                                  const float* bias2, int relu, float* out, long long o_bs, int o_st, int B,
+                                  void* stream) {
+  if (!ia || !A || !ib || !B_ || !scale || !bias || !out) return KRRN_EARG;
+  if (n < 1 || C < 1 || B < 1) return KRRN_ESHAPE;
+  if ((C & 3) || (a_st & 3) || (b_st & 3) || (o_st & 3) || (a_bs & 3) || (b_bs & 3) || (o_bs & 3) ||
+      !krrn_aligned16(A) || !krrn_aligned16(B_) || !krrn_aligned16(out) || !krrn_aligned16(scale) ||
+      !krrn_aligned16(bias) || (bias2 && !krrn_aligned16(bias2)))
+    return KRRN_EALIGN;
+  const long long total = (long long)B * n * (C / 4);
+  if (total < 0x7fffffffLL)
+    hipLaunchKernelGGL(gather2_add_kernel<int>, grid1(total), dim3(256), 0, (hipStream_t)stream, ia, A, a_bs, a_st, ib,
+                       B_, b_bs, b_st, n, C / 4, scale, bias, bias2, relu, out, o_bs, o_st, (int)total);
+  else
+    hipLaunchKernelGGL(gather2_add_kernel<long long>, grid1(total), dim3(256), 0, (hipStream_t)stream, ia, A, a_bs,
+                       a_st, ib, B_, b_bs, b_st, n, C / 4, scale, bias, bias2, relu, out, o_bs, o_st, total);
   return krrn_launch_status();
 }

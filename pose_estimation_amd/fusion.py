@@ -87,6 +87,9 @@ class FusionNetLite(nn.Module):
         self.conv_5 = Conv_fuse_layer(512, 512, S)
 
 
+
+FEAT_SID = 4  # plan stream of the materialised output concat (joined by the caller)
+
 def level_sizes(N: int, k0: int):
     N1 = int(N / 4)
     N2 = int(N1 / 4)
@@ -217,14 +220,18 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     gemm(fm4, 512, 0, B * N2, fu.conv_5, Y5)
     gcn(idx2, N2, k2, off(PV2, 0), N2 * 9, 9, _dn(fu.conv_5.directions, dev), 512, Y5, None, False,
         off(fm5, 0), N2 * 512, 512)
-    # the 1280-wide concat (fusion.py:234-238)
+    # the 1280-wide concat (fusion.py:234-238). TBase consumes it by linearity from the level rows
+    # (posenet.build_tbase_plan), so the materialised concat (the module's output, kept for
+    # inspection) is written on side stream FEAT_SID, off the critical path; the caller joins it.
     plan.join([3])
-    plan.add("krrn_gather_rows_f32", ptr(nn2), 0, N, N, off(fm5, 0), N2 * 512, 512, off(feat, 0), N * 1280, 1280,
-             512, B)
-    plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat1, 0), N * 384, 384, off(feat, 512), N * 1280, 1280,
-             384, B)
-    plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat2, 0), N1 * 384, 384, off(feat, 896), N * 1280, 1280,
-             384, B)
+    plan.fork([FEAT_SID])
+    with plan.on_stream(FEAT_SID):
+        plan.add("krrn_gather_rows_f32", ptr(nn2), 0, N, N, off(fm5, 0), N2 * 512, 512, off(feat, 0), N * 1280, 1280,
+                 512, B)
+        plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat1, 0), N * 384, 384, off(feat, 512), N * 1280,
+                 1280, 384, B)
+        plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat2, 0), N1 * 384, 384, off(feat, 896), N * 1280,
+                 1280, 384, B)
     plan.buffers.append(keep)
     return feat, dict(pool_v=nb4["v"], pool_x=nb4["x"], pool_n=nb4["n"], pool2=nb4b, idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1, nn2=nn2, feat1=feat1, feat2=feat2, fm5=fm5,
                       F0=F0, V1=V1, PV1=PV1, PV2=PV2, FP1=FP1, FP2=FP2, fm4=fm4)

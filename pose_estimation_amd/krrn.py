@@ -29,7 +29,7 @@ import torch.nn as nn
 
 from . import ops
 from .config import CONFIG
-from .fusion import FusionNetLite, build_fusion_plan, level_sizes
+from .fusion import FEAT_SID, FusionNetLite, build_fusion_plan, level_sizes
 from .hrnet import _Builder, build_hrnet, build_hrnet_plan
 from .ops import Act, pad4
 from .posenet import PoseNet, build_tbase_plan
@@ -118,8 +118,12 @@ class KRRNPlan:
                 self.device_perm_plan.add("krrn_randperm_i32", ptr(self.seed), sid, n, m, 1, ptr(self.perms[k]))
             feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms)
             self.feat = feat
+            fb = self.fusion_bufs
+            levels = dict(fm5=fb["fm5"], feat1=fb["feat1"], feat2=fb["feat2"], nn1=fb["nn1"], nn2=fb["nn2"], N1=N1,
+                          N2=N2)
             self.pred_t, self.tbase_bufs = build_tbase_plan(model.pose.t_net, plan, B, N, feat, "cls", "cloud",
-                                                            cfg.Module.POSENet.INC_R, C)
+                                                            cfg.Module.POSENet.INC_R, C, levels=levels)
+            plan.join([FEAT_SID])
         if pose_hook is not None:
             plan.join([psid])
         self.env = {"cls": self.cls, "cloud": self.cloud}

@@ -6,7 +6,8 @@ and KRRN.forward's pred_t = mean_N(p_emb + t_res) (krrn.py:153).
 
 Execution: the one-hot class channels of the concat (krrn.py:132-138) contribute exactly the
 column W1[:, 1280 + cls] to conv1, so they become a per-crop bias (one gather launch) instead
-of C extra input channels; conv1..conv3 are f32-MFMA GEMMs with BN folded into the epilogue;
+of C extra input channels; conv1 runs by linearity on the fusion's level rows (see
+build_tbase_plan); conv1..conv3 are f32-MFMA GEMMs with BN folded into the epilogue;
 conv4 + the mean over points is one reduction launch per crop.
 """
 from __future__ import annotations
@@ -40,9 +41,16 @@ class PoseNet(nn.Module):
 
 
 def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, cls_key: str, cloud_key: str,
-                     inc_r: int, num_cls: int):
+                     inc_r: int, num_cls: int, levels=None):
     """Emit TBase + pred_t. `feat` is [B, N, inc_r]; cls ([B, 1] int64) and cloud ([B, N, 3])
-    are late-bound env tensors. Returns the [B, 3] pred_t buffer."""
+    are late-bound env tensors. Returns the [B, 3] pred_t buffer.
+
+    With `levels` (the fusion's level rows fm5 [B, N2, 512], feat1 [B, N, 384], feat2 [B, N1, 384]
+    and the nearest indices nn1 / nn2 that build the concat, fusion.py:230-238), conv1 runs by
+    linearity on the level rows instead of the N gathered rows: P2 = fm5 W1[:, :512]^T (N2 rows),
+    P1 = feat1[:N1] W1[:, 512:896]^T + feat2 W1[:, 896:1280]^T (N1 rows; the reference indexes
+    feat_1 with nearest_pool_1, so only its first N1 rows are ever read), then one gather-add
+    launch applies BN + one-hot column + ReLU per point. 29 instead of 168 GFLOP at config 2."""
     dev = plan.device
     w1 = tb.conv1.weight.detach()[:, :, 0]
     spec1 = ops.make_linear(w1[:, :inc_r], tb.conv1.bias, tb.bn1, dev)
@@ -61,17 +69,37 @@ def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, 
     pred_t = plan.buf((B, 3))
     M = B * N
     plan.add("krrn_gather_rows_f32", Late(cls_key), 1, 1, 1, ptr(colv), 0, np1, ptr(b2), np1, np1, np1, B)
+    keep = [spec1, spec2, spec3, colv, w4, b4]
 
-    def gemm(a, K, spec, out, bias2=None):
+    def gemm(a, K, spec, out, bias2=None, rows=M, relu=True):
         np_ = ops.pad4(spec.cout)
-        add_conv(plan, x=ptr(a), x_cs=K, x_co=0, B=1, Hi=1, Wi=M, cin_p=spec.cin_p, Hg=1, Wg=M, in_s=1, taps=[(0, 0)],
-                 wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
+        add_conv(plan, x=ptr(a), x_cs=K, x_co=0, B=1, Hi=1, Wi=rows, cin_p=spec.cin_p, Hg=1, Wg=rows, in_s=1,
+                 taps=[(0, 0)], wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
                  bias2=ptr(bias2) if bias2 is not None else None, b2_div=N, out=ptr(out), out_cs=out.shape[-1],
-                 out_co=0, Ho=1, Wo=M, relu=True, cin=spec.cin, cout=spec.cout, tag="tbase_gemm")
+                 out_co=0, Ho=1, Wo=rows, relu=relu, cin=spec.cin, cout=spec.cout, tag="tbase_gemm")
 
-    gemm(feat, inc_r, spec1, h1, bias2=b2)
+    if levels is None:
+        gemm(feat, inc_r, spec1, h1, bias2=b2)
+    else:
+        N1, N2 = levels["N1"], levels["N2"]
+        wa = ops.make_linear(w1[:, 0:512], None, None, dev)
+        wb = ops.make_linear(w1[:, 512:896], None, None, dev)
+        wc = ops.make_linear(w1[:, 896:1280], None, None, dev)
+        keep += [wa, wb, wc]
+        P2 = plan.buf((B * N2, np1))
+        Q = plan.buf((B * N1, np1))
+        P1 = plan.buf((B * N1, np1))
+        gemm(levels["fm5"], 512, wa, P2, rows=B * N2, relu=False)
+        gemm(levels["feat2"], 384, wc, Q, rows=B * N1, relu=False)
+        # feat1 rows 0..N1-1 of every crop (grid B x N1 over images of N points), + Q
+        add_conv(plan, x=ptr(levels["feat1"]), x_cs=384, x_co=0, B=B, Hi=1, Wi=N, cin_p=wb.cin_p, Hg=1, Wg=N1,
+                 in_s=1, taps=[(0, 0)], wt=ptr(wb.wt[0]), N=np1, n_store=np1, scale=ptr(wb.scale), bias=ptr(wb.bias),
+                 res=ptr(Q), res_cs=np1, res_co=0, out=ptr(P1), out_cs=np1, out_co=0, Ho=1, Wo=N1, relu=False,
+                 cin=wb.cin, cout=wb.cout, tag="tbase_gemm")
+        plan.add("krrn_gather2_add_f32", ptr(levels["nn2"]), ptr(P2), N2 * np1, np1, ptr(levels["nn1"]), ptr(P1),
+                 N1 * np1, np1, N, np1, ptr(spec1.scale), ptr(spec1.bias), ptr(b2), 1, ptr(h1), N * 1024, 1024, B)
     gemm(h1, 1024, spec2, h2)
     gemm(h2, 256, spec3, h3)
     plan.add("krrn_tbase_tail_f32", ptr(h3), B, N, 256, ptr(w4), ptr(b4), Late(cloud_key), ptr(pred_t), ptr(None))
-    plan.buffers.append([spec1, spec2, spec3, colv, w4, b4])
+    plan.buffers.append(keep)
     return pred_t, dict(h1=h1, h2=h2, h3=h3)

@@ -36,6 +36,7 @@ _lib.register("krrn_heads_select_f32", [P, I, I, P, I, P, P, P, I, I, I, P])
 _lib.register("krrn_points_gather_f32", [P, P, P, P, I, I, I, I, P, P])
 _lib.register("krrn_gather_rows_f32", [P, I, L, I, P, L, I, P, L, I, I, I, P])
 _lib.register("krrn_tbase_tail_f32", [P, I, I, I, P, P, P, P, P, P])
+_lib.register("krrn_gather2_add_f32", [P, P, L, I, P, P, L, I, I, I, P, P, P, I, P, L, I, I, P])
 _lib.register("krrn_pnp_ransac_f32", [P, I, P, I, P, I, P, P, P, P, P, P, I, F, P, P, P, P, P, I, P])
 _lib.register("krrn_randperm_i32", [P, U, I, I, I, P, P])
 _lib.register("krrn_ransac_subsets", [P, U, I, I, I, P, P])
