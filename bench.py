@@ -29,7 +29,7 @@ import torch.distributed as dist  # noqa: E402
 from pose_estimation_amd import distributed as kd  # noqa: E402
 from pose_estimation_amd.config import make_config  # noqa: E402
 from pose_estimation_amd.krrn import KRRN  # noqa: E402
-from pose_estimation_amd.pipeline import BatchPipeline  # noqa: E402
+from pose_estimation_amd.pipeline import BatchPipeline, PipelinedPipeline  # noqa: E402
 from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
 
 METRIC = "crops/sec at 640×480 RGB-D, 1000 sampled pts; ADD(-S) AUC vs reference"
@@ -142,6 +142,9 @@ def main():
     ap.add_argument("--micro", type=int, default=1,
                     help="micro-batches processed concurrently inside each step (pipeline.py)")
     ap.add_argument("--flat", action="store_true", help="no plan side streams inside a micro-batch")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="two-stage pipeline (pipeline.PipelinedPipeline): the backbone of batch k+1 beside "
+                         "heads / fusion / PnP of batch k; default: one batch per step end to end")
     args = ap.parse_args()
 
     rank, world, local = kd.init_from_env("nccl")
@@ -155,7 +158,10 @@ def main():
     model = model.to(dev).eval()
     model.perm_mode = "device"
     data = make_batch(B, S, N, seed=1 + rank)
-    step = BatchPipeline(model, B, S, N, dev, parts=args.micro, seed=rank, inner_streams=not args.flat)
+    if not args.pipeline or args.micro > 1:
+        step = BatchPipeline(model, B, S, N, dev, parts=args.micro, seed=rank, inner_streams=not args.flat)
+    else:
+        step = PipelinedPipeline(model, B, S, N, dev, seed=rank)
     step.load(data)
     record = torch.zeros((B, kd.RECORD), dtype=torch.float32, device=dev)
 
@@ -167,8 +173,8 @@ def main():
     def one_step():
         step.step()
         if world > 1:
-            for pt in step.parts:
-                kd.pack_records(pt.R, pt.t, pt.kp.pred_t, pt.inl, out=record[pt.lo:pt.hi])
+            r = step.results()  # the batch this step completed
+            kd.pack_records(r["R"], r["t"], r["pred_t"], r["inliers"], out=record)
             kd.gather_records(record)
 
     for _ in range(args.warmup):
@@ -210,7 +216,10 @@ def main():
                                    f"HRNet-{args.backbone.upper()} + {N}-pt fusion + TBase, PnP-RANSAC (H=100) on GPU",
                        "batch_per_gpu": B, "crop": S, "points": N, "backbone": f"hrnet_{args.backbone}",
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": step.graph is not None,
-                       "micro_batches": args.micro},
+                       "micro_batches": args.micro,
+                       "pipeline": "none" if isinstance(step, BatchPipeline) else
+                       "2-stage (backbone of batch k+1 beside heads/fusion/PnP of batch k; "
+                       "one batch completes per step)"},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -58,6 +58,11 @@ class KRRNPlan:
         xa = Act(plan.buf((B, S, S, 4)), B, S, S, 4, 0, 3)
         plan.add("krrn_nchw_to_nhwc_f32", ptr(self.x_in), B, 3, S, S, ptr(xa.t), 4, 0)
         xmap, ymap, specs = build_hrnet_plan(model.backbone, plan, xa)
+        # ops[:split] = the backbone (all its side streams joined); ops[split:] read only xmap / ymap
+        # of it (plus the static inputs), which lets BatchPipeline(pipelined=True) overlap a batch's
+        # backbone with the previous batch's heads / fusion / pose
+        self.split = len(plan.ops)
+        self.backbone_out = (xmap.t, ymap.t)
         bld = _Builder(plan, B)
         # the two head towers are independent until the class select: NMLNet on stream 1
         plan.fork([1])

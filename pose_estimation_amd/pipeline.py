@@ -14,8 +14,9 @@ crop of the batch is still processed exactly once per step, with the same per-cr
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -71,7 +72,8 @@ class BatchPipeline:
         self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)] if parts > 1 else []
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         # parts > 1 runs each part's plan serially on its part stream: capturing nested plan side
-        # streams under per-part streams segfaults in hipStreamEndCapture (measured on ROCm 7.2)
+        # streams under per-part streams segfaults in hipStreamEndCapture (measured on ROCm 7.2,
+        # also when every side stream first joins the capture through the origin stream)
         self.inner_streams = inner_streams and parts == 1
 
     # -- inputs / outputs ------------------------------------------------------------------
@@ -150,3 +152,126 @@ class BatchPipeline:
         for p, env in self.plans():
             out.extend(p.run_timed(dict(env)))
         return out
+
+
+# ------------------------------------------------------------------------------------------
+# Two-stage software pipeline across batches
+# ------------------------------------------------------------------------------------------
+def _sub_plan(plan: Plan, lo: int, hi: int) -> Plan:
+    """A view of plan.ops[lo:hi] sharing the plan's side streams."""
+    sub = Plan(plan.device)
+    sub.ops, sub.nstreams, sub._side = plan.ops[lo:hi], plan.nstreams, plan._side
+    return sub
+
+
+class PipelinedPipeline:
+    """BatchPipeline's step as a two-stage software pipeline over two batch slots.
+
+    Stage A = the HRNet backbone (KRRNPlan.ops[:split]: ~430 small, latency-bound convs that
+    leave most CUs idle), stage B = heads + fusion + TBase + PnP (KRRNPlan.ops[split:] plus the
+    device draws and the pose plan). Half-step h runs B of slot h on the caller's stream while A
+    of slot 1-h runs on a side stream; each stage of each slot is its own hipGraph (one capture
+    per stage: capturing both into one graph would need side streams forking side streams, which
+    segfaults in hipStreamEndCapture on ROCm 7.2), and a half-step replays two of them on two
+    streams. In steady state every half-step completes one whole batch (`results()`); a crop's
+    math is unchanged (same kernels, per-slot buffers), only its latency is two half-steps.
+    """
+
+    def __init__(self, model: KRRN, B: int, S: int, N: int, device, seed: int = 0):
+        self.B, self.S, self.N, self.device = B, S, N, torch.device(device)
+        self.slots = [BatchPipeline(model, B, S, N, device, parts=1, seed=2 * seed + i) for i in range(2)]
+        self.stage_a: List[Tuple[Plan, dict]] = []
+        self.stage_b: List[List[Tuple[Plan, dict]]] = []
+        for sl in self.slots:
+            pt = sl.parts[0]
+            kp = pt.kp
+            self.stage_a.append((_sub_plan(kp.plan, 0, kp.split), kp.env))
+            self.stage_b.append([(kp.device_perm_plan, {}), (_sub_plan(kp.plan, kp.split, len(kp.plan.ops)), kp.env),
+                                 (pt.pose, {})])
+        # stage A's stream priority (KRRN_PIPE_PRIO, e.g. -1 = high): its latency-bound chain is
+        # the one to keep moving while stage B's big grids occupy the CUs
+        self.side = torch.cuda.Stream(self.device, priority=int(os.environ.get("KRRN_PIPE_PRIO", "0")))
+        self.graphs_a: List[Optional[torch.cuda.CUDAGraph]] = [None, None]
+        self.graphs_b: List[Optional[torch.cuda.CUDAGraph]] = [None, None]
+        self.h = 0
+        self.primed = False
+
+    def load(self, data):
+        for s in self.slots:
+            s.load(data)
+
+    def _run_a(self, slot: int):
+        p, env = self.stage_a[slot]
+        p.run(dict(env))
+
+    def _run_b(self, slot: int):
+        for p, env in self.stage_b[slot]:
+            p.run(dict(env))
+
+    def _prime(self):
+        """Stage A of both slots once, so the first half-step's stage B has backbone features."""
+        for i in range(2):
+            self._run_a(i)
+        self.primed = True
+
+    def _half(self, run_a, run_b):
+        b, a = self.h, self.h ^ 1
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            run_a(a)
+        run_b(b)
+        main.wait_stream(self.side)
+        self.h ^= 1
+
+    def run(self):
+        if not self.primed:
+            self._prime()
+        self._half(self._run_a, self._run_b)
+
+    def capture(self):
+        """Warm up every stage once on a side stream, then capture one hipGraph per stage and slot."""
+        if not self.primed:
+            self._prime()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for i in range(2):
+                self._run_b(i)
+                self._run_a(i)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        for i in range(2):
+            for gs, fn in ((self.graphs_b, self._run_b), (self.graphs_a, self._run_a)):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    fn(i)
+                gs[i] = g
+        torch.cuda.synchronize(self.device)
+        # the captures above do not execute: slot state is as after the warm-up (A of both slots
+        # last), so the next half-step's stage B (slot 0) reads valid features
+        self.h = 0
+
+    def step(self):
+        if self.graphs_a[0] is None:
+            self.run()
+            return
+        self._half(lambda i: self.graphs_a[i].replay(), lambda i: self.graphs_b[i].replay())
+
+    def results(self):
+        """The batch completed by the most recent half-step."""
+        return self.slots[self.h ^ 1].results()
+
+    def plans(self):
+        return self.slots[0].plans()
+
+    def profile(self):
+        return self.slots[0].profile()
+
+    @property
+    def graph(self):
+        return self.graphs_a[0]
+
+    @property
+    def parts(self):
+        return self.slots[0].parts

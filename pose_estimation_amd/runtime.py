@@ -170,10 +170,14 @@ class Plan:
             if s != 0:
                 self.ops.append(Sync(s, 0))
 
-    def _streams(self, env: Dict[str, Any], serial: bool):
-        main = torch.cuda.current_stream(self.device)
+    def side_streams(self) -> List[torch.cuda.Stream]:
         while len(self._side) < self.nstreams - 1:
             self._side.append(torch.cuda.Stream(self.device))
+        return self._side
+
+    def _streams(self, env: Dict[str, Any], serial: bool):
+        main = torch.cuda.current_stream(self.device)
+        self.side_streams()
         streams = [main] + self._side
         for sid in range(self.nstreams):
             env[_skey(sid)] = P((main if serial else streams[sid]).cuda_stream)
