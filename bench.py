@@ -37,6 +37,30 @@ PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f3
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
+# compulsory fusion HBM bytes per crop (fp32 features, int32 indices; each GCN
+# GEMM output written once and read once, every other tensor read or written once)
+FUSION_BYTES_PER_CROP = {1000: 49.7e6, 4096: 202.6e6}
+
+
+def fusion_roofline(prof, fusion_ids, B: int, N: int):
+    """FusionNetLite as one unit: algorithmic bytes / serial device time of
+    its launches vs the HBM peak (north_star target >= 40 %), and the GCN GEMMs' MFMA rate."""
+    ops = [(op, ms) for op, ms in prof if id(op) in fusion_ids]
+    if not ops:
+        return None
+    ms = sum(t for _, t in ops)
+    gemm_ms = sum(t for op, t in ops if op.meta.get("flops"))
+    gemm_fl = sum(op.meta.get("flops", 0.0) for op, _ in ops)
+    per_crop = FUSION_BYTES_PER_CROP.get(N)
+    out = {"ms_per_step": round(ms, 3), "launches": len(ops), "gemm_ms": round(gemm_ms, 3),
+           "gemm_TFLOP/s": round(gemm_fl / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else None}
+    if per_crop:
+        gbs = per_crop * B / (ms * 1e-3) / 1e9
+        out.update({"bound": "hbm", "bytes_per_crop": per_crop, "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4)})
+    return out
+
+
 def roofline_from_profile(prof, B: int):
     groups = {}
     for op, ms in prof:
@@ -53,6 +77,8 @@ def roofline_from_profile(prof, B: int):
     achieved = (g["flops"] / g["n"]) / (avg_ms * 1e-3) / 1e12 if g["flops"] > 0 else None
     conv_ms = sum(v["ms"] for k, v in groups.items() if k.startswith("conv_gemm"))
     conv_fl = sum(v["flops"] for k, v in groups.items() if k.startswith("conv_gemm"))
+    allc = [v for k, v in groups.items() if k.startswith("conv_gemm") or k.startswith("wino")]
+    allc_ms, allc_fl, allc_mf = (sum(v[f] for v in allc) for f in ("ms", "flops", "mfma"))
     breakdown = {k: {"ms": round(v["ms"], 4), "launches": v["n"],
                      **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {})}
                  for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])}
@@ -66,6 +92,12 @@ def roofline_from_profile(prof, B: int):
             "all_conv_gemm": {"ms_per_step": round(conv_ms, 3),
                               "TFLOP/s": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2) if conv_ms else None,
                               "GFLOP_per_crop": round(conv_fl / B / 1e9, 3)},
+            "all_conv": {"ms_per_step": round(allc_ms, 3), "GFLOP_per_crop": round(allc_fl / B / 1e9, 3),
+                         "TFLOP/s": round(allc_fl / (allc_ms * 1e-3) / 1e12, 2) if allc_ms else None,
+                         "frac": round(allc_fl / (allc_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4) if allc_ms else None,
+                         "mfma_pipe_frac": round(allc_mf / (allc_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)
+                         if allc_ms else None,
+                         "note": "every conv / GEMM of the step incl. Winograd, direct-conv FLOPs (SURVEY §8d)"},
             "events_ms_per_step": round(total_ms, 3)}
     if g["mfma"] and abs(g["mfma"] - g["flops"]) > 1e-6 * g["flops"]:
         # Winograd: `achieved` counts the direct-conv FLOPs the launch replaces (SURVEY §8d's
@@ -200,7 +232,10 @@ def main():
     roof, breakdown = None, None
     if rank == 0 and not args.no_profile:
         step.profile()  # warm the eager path once
-        roof, breakdown = roofline_from_profile(step.profile(), B)
+        prof = step.profile()
+        roof, breakdown = roofline_from_profile(prof, B)
+        fids = set().union(*(getattr(pt.kp, "fusion_op_ids", set()) for pt in step.parts))
+        roof["fusion"] = fusion_roofline(prof, fids, B, N)
         if args.breakdown:
             with open(args.breakdown, "w") as f:
                 json.dump({"roofline": roof, "kernels": breakdown}, f, indent=1)

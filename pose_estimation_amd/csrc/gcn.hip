@@ -201,29 +201,31 @@ KRRN_API int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, cons
 namespace {
 
 constexpr int kGcnThreads = 256;
-constexpr int kGcnPts = 8;  // points per block: 32 lanes x 4 channels each per point
 constexpr int kGcnKmax = 16;
 
-// Block = 8 points of one crop; a point is 32 lanes, lane l owning channels 4l.. (+128 per
-// step for C = 512). For each support s and neighbour j a lane reads one float4 of the
-// neighbour's Y row (512-B coalesced per point), so every neighbour row segment
-// Y[nj, C + s*C : C + (s+1)*C] is one wide read. The block -> (crop, points) map is XCD-aware:
-// consecutive point groups of one crop share an XCD and its L2, where their overlapping
-// neighbourhoods (choose is pixel-ordered, so neighbours have nearby indices) hit.
-// KC = compile-time k (0: runtime k).
-template <int D, bool HAS_Y, int KC>
+// Block = 256 / LP points of one crop; a point is LP lanes, lane l owning channels 4l.. (+4 LP
+// per step when C > 4 LP). LP = 32 for C = 128 (levels 0 / 1: 8 points per block), LP = 128 for
+// C = 512 (level 2: 2 points per block, so each lane walks one channel group instead of four —
+// that path is gather-latency bound, 62 points per crop). For each support s and neighbour j a
+// lane reads one float4 of the neighbour's Y row (16 LP-byte coalesced per point), so every
+// neighbour row segment Y[nj, C + s*C : C + (s+1)*C] is one wide read. The block -> (crop,
+// points) map is XCD-aware: consecutive point groups of one crop share an XCD and its L2, where
+// their overlapping neighbourhoods (choose is pixel-ordered, so neighbours have nearby indices)
+// hit. KC = compile-time k (0: runtime k).
+template <int D, bool HAS_Y, int KC, int LP>
 __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
     const int* __restrict__ idx, int n, int k, const float* __restrict__ v, long long v_bs, int v_st,
     const float* __restrict__ dn, int S, int C, const float* __restrict__ Y,
     const float* __restrict__ bn_s, const float* __restrict__ bn_b, int relu, float* __restrict__ out,
     long long o_bs, int o_st) {
-  __shared__ float sdir[kGcnPts * kGcnKmax * D];
-  __shared__ int snb[kGcnPts * kGcnKmax];
+  constexpr int kPts = kGcnThreads / LP;
+  __shared__ float sdir[kPts * kGcnKmax * D];
+  __shared__ int snb[kPts * kGcnKmax];
   const int gx = gridDim.x;
   const int lin = krrn_xcd_remap(blockIdx.x + gx * blockIdx.y, gx * gridDim.y);
   const int b = lin / gx;
-  const int p0 = (lin - b * gx) * kGcnPts;
-  const int np = min(kGcnPts, n - p0);
+  const int p0 = (lin - b * gx) * kPts;
+  const int np = min(kPts, n - p0);
   const int kk = KC ? KC : k;
   const float* vb = v + b * v_bs;
   // 1) neighbour directions, F.normalize(v[j] - v[i], dim=-1) (gcn3d.py:60-69)
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
     for (int i = 0; i < D; ++i) sdir[(p * kGcnKmax + j) * D + i] = dv[i] / nr;
   }
   __syncthreads();
-  const int p = threadIdx.x >> 5, l = threadIdx.x & 31;
+  const int p = threadIdx.x / LP, l = threadIdx.x % LP;
   if (p >= np) return;
   const int pi = p0 + p;
   const int SC = S * C;
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
   const float* yb = HAS_Y ? Y + b * (long long)n * yrow : nullptr;
   const float* dp = sdir + p * kGcnKmax * D;
   const int* nbp = snb + p * kGcnKmax;
-  for (int c = 4 * l; c < C; c += 128) {
+  for (int c = 4 * l; c < C; c += 4 * LP) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < S; ++s) {
       f32x4 w[D];
@@ -298,11 +300,16 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   if (k < 1 || k > kGcnKmax || n < 1 || S < 1 || C < 1 || B < 1) return KRRN_ESHAPE;
   if ((C & 3) || (o_st & 3) || (o_bs & 3) || !krrn_aligned16(out) || !krrn_aligned16(dn)) return KRRN_EALIGN;
   if (Y && !krrn_aligned16(Y)) return KRRN_EALIGN;
-  dim3 grid(krrn_cdiv(n, kGcnPts), B);
+  const bool wide = C >= 512;  // LP = 128 lanes per point (see the kernel comment)
+  dim3 grid(krrn_cdiv(n, wide ? kGcnThreads / 128 : kGcnThreads / 32), B);
   hipStream_t s = (hipStream_t)stream;
-#define KRRN_GCN_LAUNCH(DD, HY, KC)                                                                         \
-  hipLaunchKernelGGL((gcn_conv_kernel<DD, HY, KC>), grid, dim3(kGcnThreads), 0, s, idx, n, k, v, v_bs, v_st, \
-                     dn, S, C, Y, bn_scale, bn_bias, relu, out, o_bs, o_st)
+#define KRRN_GCN_LAUNCH(DD, HY, KC)                                                                        \
+  if (wide)                                                                                                \
+    hipLaunchKernelGGL((gcn_conv_kernel<DD, HY, KC, 128>), grid, dim3(kGcnThreads), 0, s, idx, n, k, v,   \
+                       v_bs, v_st, dn, S, C, Y, bn_scale, bn_bias, relu, out, o_bs, o_st);                 \
+  else                                                                                                     \
+    hipLaunchKernelGGL((gcn_conv_kernel<DD, HY, KC, 32>), grid, dim3(kGcnThreads), 0, s, idx, n, k, v,    \
+                       v_bs, v_st, dn, S, C, Y, bn_scale, bn_bias, relu, out, o_bs, o_st)
 #define KRRN_GCN_K(DD, HY)                 \
   if (k == 10) KRRN_GCN_LAUNCH(DD, HY, 10); \
   else if (k == 7) KRRN_GCN_LAUNCH(DD, HY, 7); \

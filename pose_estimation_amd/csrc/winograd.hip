@@ -33,7 +33,15 @@
 namespace {
 
 constexpr int kWT = 32;       // tiles per block
-constexpr int kWN = 64;       // output channels per block
+#ifndef KRRN_WINO_WN
+#define KRRN_WINO_WN 64
+#endif
+constexpr int kWN = KRRN_WINO_WN;  // output channels per block
+constexpr int kNJ = kWN / 32;      // 32-wide n-blocks per wave
+constexpr int kN4 = kWN / 4;       // 4-channel groups per tile
+constexpr int kNP = kWT * kN4 / 256;      // epilogue (tile, 4-channel) pairs per thread
+constexpr int kNWF = 16 * kWN * 2 / 256;  // weight float4s staged per thread per chunk
+constexpr int kWBlocks = kWN == 64 ? 2 : 3;  // blocks per CU the LDS footprint allows
 constexpr int kWC = 8;        // input channels per chunk
 constexpr int kWP = kWC + 4;  // LDS row pitch (floats): 3 x 16 B
 constexpr unsigned kWOOB = 0xFFFF0000u;  // > any valid offset, and + channel offsets stays > it
@@ -64,12 +72,12 @@ struct WinoArgs {
 constexpr int kSP = kWN + 4;
 static_assert(4 * 2 * kWT * kSP <= 16 * (kWT + kWN) * kWP, "epilogue staging must fit the main-loop LDS");
 
-__device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][2]) {
+__device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][kNJ]) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 31;
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < kNJ; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -83,14 +91,14 @@ __device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][2])
 __device__ __forceinline__ void wino_epi_finish(const WinoArgs& a, const float* smem, int t0, int n0, int HWt) {
   const int tid = threadIdx.x;
   // geometry of this thread's 2 (tile, 4-channel) pairs and their scale / bias
-  int pt[2], pn[2];
-  size_t ppix[2][4];
-  bool pok[2], qok[2][4];
-  f32x4 scl[2], bia[2];
+  int pt[kNP], pn[kNP];
+  size_t ppix[kNP][4];
+  bool pok[kNP], qok[kNP][4];
+  f32x4 scl[kNP], bia[kNP];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kNP; ++i) {
     const int pr = tid + 256 * i;
-    const int n4 = pr & 15, tl = pr >> 4;
+    const int n4 = pr % kN4, tl = pr / kN4;
     pt[i] = tl;
     pn[i] = n0 + 4 * n4;
     const int t = t0 + tl;
@@ -112,7 +120,7 @@ __device__ __forceinline__ void wino_epi_finish(const WinoArgs& a, const float* 
     }
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kNP; ++i) {
     if (!pok[i]) continue;
     const int tl = pt[i], n = pn[i];
     const int n4 = (n - n0) >> 2;
@@ -156,7 +164,7 @@ __device__ __forceinline__ void wino_epi_finish(const WinoArgs& a, const float* 
   }
 }
 
-__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f32x16 (&acc)[4][2], int t0, int n0,
+__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f32x16 (&acc)[4][kNJ], int t0, int n0,
                                               int HWt) {
   wino_epi_stage(smem, acc);
   wino_epi_finish(a, smem, t0, n0, HWt);
@@ -169,7 +177,7 @@ __device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f3
 struct WinoStager {
   __amdgpu_buffer_rsrc_t rsA, rsU;
   unsigned poff[16];  // byte offset of patch pixel (r, c), channel sc; kWOOB outside the image
-  unsigned woff[8];   // byte offset of this thread's 8 weight float4s at chunk 0
+  unsigned woff[kNWF];  // byte offset of this thread's weight float4s at chunk 0
   unsigned wstride;   // bytes per weight chunk
   int st, sc, cin, nchunks;
 
@@ -203,16 +211,16 @@ struct WinoStager {
       }
     // U is chunk-major [chunk][xi][N][8]: one chunk of one block is 16 contiguous 2 KB runs
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e = tid + 256 * i;  // (xi, n, c4) over 16 x 64 x 2
-      const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
+    for (int i = 0; i < kNWF; ++i) {
+      const int e = tid + 256 * i;  // (xi, n, c4) over 16 x kWN x 2
+      const int xi = e / (2 * kWN), n = (e >> 1) % kWN, c4 = e & 1;
       woff[i] = (n0 + n < a.N) ? (unsigned)((((long long)xi * a.N + n0 + n) * kWC + 4 * c4) * 4) : kWOOB;
     }
     wstride = (unsigned)(16 * a.N * kWC * 4);
   }
 
   // chunks past the last one load zeros (out-of-range buffer offsets), branch-free
-  __device__ __forceinline__ void load(int ck, float (&d)[16], f32x4 (&w)[8]) const {
+  __device__ __forceinline__ void load(int ck, float (&d)[16], f32x4 (&w)[kNWF]) const {
     const int c0 = ck * kWC;
     const unsigned cb = (unsigned)c0 * 4u;
     const unsigned cmask = (c0 + sc < cin) ? 0u : kWOOB;
@@ -222,11 +230,11 @@ struct WinoStager {
     const unsigned wmask = (ck < nchunks) ? 0u : kWOOB;  // padded channels of the last chunk are zero in U
     const unsigned wb = (unsigned)ck * wstride;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < kNWF; ++i)
       w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, (woff[i] + wb) | wmask, 0, 0));
   }
 
-  __device__ __forceinline__ void stage(const float (&d)[16], const f32x4 (&w)[8], float* As, float* Bs) const {
+  __device__ __forceinline__ void stage(const float (&d)[16], const f32x4 (&w)[kNWF], float* As, float* Bs) const {
     // V = B^T d B
     float t[16];
 #pragma unroll
@@ -245,30 +253,34 @@ struct WinoStager {
     }
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < kNWF; ++i) {
       const int e = tid + 256 * i;
-      const int xi = e >> 7, n = (e >> 1) & 63, c4 = e & 1;
+      const int xi = e / (2 * kWN), n = (e >> 1) % kWN, c4 = e & 1;
       *reinterpret_cast<f32x4*>(Bs + (xi * kWN + n) * kWP + 4 * c4) = w[i];
     }
   }
 };
 
-// Wave w owns components xi = 4w .. 4w+3 over the 32 x 64 block: per chunk 32 MFMAs.
-__device__ __forceinline__ void wino_mma(const float* As, const float* Bs, f32x16 (&acc)[4][2]) {
+// Wave w owns components xi = 4w .. 4w+3 over the 32 x 64 block: per chunk 32 MFMAs. All 12
+// operand fragments are read first; the k-step s is the OUTER loop so consecutive MFMAs write
+// 8 different accumulators (no back-to-back dependent accumulator).
+__device__ __forceinline__ void wino_mma(const float* As, const float* Bs, f32x16 (&acc)[4][kNJ]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 31, fk = (lane >> 5) * 4;
+  f32x4 av[4], bv[4][kNJ];
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
     const int xi = 4 * wave + x;
-    const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
+    av[x] = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
-    }
+    for (int j = 0; j < kNJ; ++j) bv[x][j] = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
   }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j) acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x][s], bv[x][j][s], acc[x][j], 0, 0, 0);
 }
 
 __device__ __forceinline__ void wino_block(const WinoArgs& a, int& t0, int& n0, int& HWt) {
@@ -282,22 +294,22 @@ __device__ __forceinline__ void wino_block(const WinoArgs& a, int& t0, int& n0, 
 
 // Single LDS buffer (73.5 KB) -> 2 blocks per CU; one block's staging overlaps the
 // other's MFMAs, the next chunk's global loads are in flight during the current MFMAs.
-__global__ __launch_bounds__(256, 2) void wino_f23_kernel(const WinoArgs a) {
+__global__ __launch_bounds__(256, kWBlocks) void wino_f23_kernel(const WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[16 * (kWT + kWN) * kWP];
   float* As = smem;                   // [xi][tile][c]
   float* Bs = smem + 16 * kWT * kWP;  // [xi][n][c]
   int t0, n0, HWt;
   wino_block(a, t0, n0, HWt);
   const WinoStager sg(a, t0, n0, HWt);
-  f32x16 acc[4][2];
+  f32x16 acc[4][kNJ];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < kNJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
   float d[16];
-  f32x4 w[8];
+  f32x4 w[kNWF];
   sg.load(0, d, w);
   for (int ck = 0; ck < sg.nchunks; ++ck) {
     sg.stage(d, w, As, Bs);

@@ -22,6 +22,8 @@ Outputs are views of plan-owned buffers that the next forward of the same shape 
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -41,6 +43,7 @@ class KRRNPlan:
 
     # side stream of the pose step when it is fused into the forward plan (pose_hook)
     POSE_SID = 6
+    POSE_AT = os.environ.get("KRRN_POSE_AT", "level1")  # measured: level1 16.68, heads 16.80, level2 16.80 ms/step
 
     def __init__(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device, pose_hook=None,
                  pose_stream: bool = True):
@@ -103,12 +106,20 @@ class KRRNPlan:
         self.specs = [specs, bld.specs]
         self.pred_t = None
         psid = self.POSE_SID if pose_stream else 0
-        if pose_hook is not None:
-            # get_pose only needs the xyz map and choose (trainer.py:403-412): it runs on its own
-            # stream beside the fusion + TBase chain and joins at the end of the plan
+
+        def emit_pose():
             plan.fork([psid])
             with plan.on_stream(psid):
                 pose_hook(self)
+
+        # get_pose only needs the xyz map and choose (trainer.py:403-412): it runs on its own
+        # stream beside the fusion + TBase chain and joins at the end of the plan. Where it forks
+        # (POSE_AT): 'heads' = right after the class select; 'level1' / 'level2' = inside the
+        # fusion, so the PnP hypothesis kernel (long-lived, 57 KB LDS per 16-lane block) overlaps
+        # the latency-bound level-2 GCN + TBase tail instead of starving the level-0 branches
+        pose_at = self.POSE_AT if (pose_hook is not None and opt_pose) else "heads"
+        if pose_hook is not None and pose_at == "heads":
+            emit_pose()
         if opt_pose:
             # choose gather (krrn.py:121-122) -> P9 = [cloud | xyz_emb | nml_emb]
             self.p9 = plan.buf((B, N, 9))
@@ -121,7 +132,11 @@ class KRRNPlan:
             self.device_perm_plan = Plan(device)
             for sid, (k, n, m) in enumerate(self.perm_sizes):
                 self.device_perm_plan.add("krrn_randperm_i32", ptr(self.seed), sid, n, m, 1, ptr(self.perms[k]))
-            feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms)
+            hooks = {pose_at: emit_pose} if pose_hook is not None and pose_at != "heads" else None
+            f0 = len(plan.ops)
+            feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms, hooks=hooks)
+            # the FusionNetLite launches (for the bench's fusion HBM roofline; pose ops excluded)
+            self.fusion_op_ids = {id(op) for op in plan.ops[f0:] if op.sid != psid and op.name != "sync"}
             self.feat = feat
             fb = self.fusion_bufs
             levels = dict(fm5=fb["fm5"], feat1=fb["feat1"], feat2=fb["feat2"], nn1=fb["nn1"], nn2=fb["nn2"], N1=N1,
