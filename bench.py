@@ -77,7 +77,7 @@ def roofline_from_profile(prof, B: int):
     achieved = (g["flops"] / g["n"]) / (avg_ms * 1e-3) / 1e12 if g["flops"] > 0 else None
     conv_ms = sum(v["ms"] for k, v in groups.items() if k.startswith("conv_gemm"))
     conv_fl = sum(v["flops"] for k, v in groups.items() if k.startswith("conv_gemm"))
-    allc = [v for k, v in groups.items() if k.startswith("conv_gemm") or k.startswith("wino")]
+    allc = [v for k, v in groups.items() if k.startswith(("conv_gemm", "conv_group", "wino"))]
     allc_ms, allc_fl, allc_mf = (sum(v[f] for v in allc) for f in ("ms", "flops", "mfma"))
     breakdown = {k: {"ms": round(v["ms"], 4), "launches": v["n"],
                      **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {})}
@@ -174,9 +174,9 @@ def main():
     ap.add_argument("--micro", type=int, default=1,
                     help="micro-batches processed concurrently inside each step (pipeline.py)")
     ap.add_argument("--flat", action="store_true", help="no plan side streams inside a micro-batch")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="two-stage pipeline (pipeline.PipelinedPipeline): the backbone of batch k+1 beside "
-                         "heads / fusion / PnP of batch k; default: one batch per step end to end")
+    ap.add_argument("--pipeline", choices=["none", "backbone", "heads"], default="none",
+                    help="two-stage pipeline (pipeline.PipelinedPipeline) split after the backbone or after the "
+                         "heads: stage A of batch k+1 runs beside stage B of batch k; none: one batch per step")
     args = ap.parse_args()
 
     rank, world, local = kd.init_from_env("nccl")
@@ -190,10 +190,10 @@ def main():
     model = model.to(dev).eval()
     model.perm_mode = "device"
     data = make_batch(B, S, N, seed=1 + rank)
-    if not args.pipeline or args.micro > 1:
+    if args.pipeline == "none" or args.micro > 1:
         step = BatchPipeline(model, B, S, N, dev, parts=args.micro, seed=rank, inner_streams=not args.flat)
     else:
-        step = PipelinedPipeline(model, B, S, N, dev, seed=rank)
+        step = PipelinedPipeline(model, B, S, N, dev, seed=rank, split=args.pipeline)
     step.load(data)
     record = torch.zeros((B, kd.RECORD), dtype=torch.float32, device=dev)
 
@@ -253,7 +253,7 @@ def main():
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": step.graph is not None,
                        "micro_batches": args.micro,
                        "pipeline": "none" if isinstance(step, BatchPipeline) else
-                       "2-stage (backbone of batch k+1 beside heads/fusion/PnP of batch k; "
+                       f"2-stage split after the {args.pipeline} (stage A of batch k+1 beside stage B of batch k; "
                        "one batch completes per step)"},
             "roofline": roof, "cpu_baseline": cpu,
         }

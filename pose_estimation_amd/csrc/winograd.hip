@@ -33,6 +33,12 @@
 namespace {
 
 constexpr int kWT = 32;       // tiles per block
+#ifndef KRRN_WINO_A2
+#define KRRN_WINO_A2 0
+#endif
+#ifndef KRRN_WINO_EXP
+#define KRRN_WINO_EXP 0
+#endif
 #ifndef KRRN_WINO_WN
 #define KRRN_WINO_WN 64
 #endif
@@ -221,17 +227,35 @@ struct WinoStager {
 
   // chunks past the last one load zeros (out-of-range buffer offsets), branch-free
   __device__ __forceinline__ void load(int ck, float (&d)[16], f32x4 (&w)[kNWF]) const {
+    loadA(ck, d);
+    loadB(ck, w);
+  }
+
+  __device__ __forceinline__ void loadA(int ck, float (&d)[16]) const {
     const int c0 = ck * kWC;
     const unsigned cb = (unsigned)c0 * 4u;
     const unsigned cmask = (c0 + sc < cin) ? 0u : kWOOB;
+#if KRRN_WINO_EXP == 1  // timing experiment: no input loads
+#pragma unroll
+    for (int p = 0; p < 16; ++p) d[p] = (float)(p + ck + sc);
+#else
 #pragma unroll
     for (int p = 0; p < 16; ++p)
       d[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, (poff[p] + cb) | cmask, 0, 0));
+#endif
+  }
+
+  __device__ __forceinline__ void loadB(int ck, f32x4 (&w)[kNWF]) const {
     const unsigned wmask = (ck < nchunks) ? 0u : kWOOB;  // padded channels of the last chunk are zero in U
     const unsigned wb = (unsigned)ck * wstride;
+#if KRRN_WINO_EXP == 2  // timing experiment: no weight loads
+#pragma unroll
+    for (int i = 0; i < kNWF; ++i) w[i] = f32x4{(float)ck, (float)i, 1.f, 2.f};
+#else
 #pragma unroll
     for (int i = 0; i < kNWF; ++i)
       w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, (woff[i] + wb) | wmask, 0, 0));
+#endif
   }
 
   __device__ __forceinline__ void stage(const float (&d)[16], const f32x4 (&w)[kNWF], float* As, float* Bs) const {
@@ -261,26 +285,29 @@ struct WinoStager {
   }
 };
 
-// Wave w owns components xi = 4w .. 4w+3 over the 32 x 64 block: per chunk 32 MFMAs. All 12
-// operand fragments are read first; the k-step s is the OUTER loop so consecutive MFMAs write
-// 8 different accumulators (no back-to-back dependent accumulator).
+// Wave w owns components xi = 4w .. 4w+3 over the 32 x 64 block: per chunk 32 MFMAs (one
+// ds_read_b128 per operand feeds 4; the s-outer order with all 12 fragments live measured equal
+// and costs 36 VGPRs).
 __device__ __forceinline__ void wino_mma(const float* As, const float* Bs, f32x16 (&acc)[4][kNJ]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 31, fk = (lane >> 5) * 4;
-  f32x4 av[4], bv[4][kNJ];
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
     const int xi = 4 * wave + x;
-    av[x] = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
+    const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
 #pragma unroll
-    for (int j = 0; j < kNJ; ++j) bv[x][j] = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
+    for (int j = 0; j < kNJ; ++j) {
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#if KRRN_WINO_EXP == 3  // timing experiment: no MFMAs
+        acc[x][j][s] += av[s] * bv[s];
+#else
+        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
+#endif
+      }
+    }
   }
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int j = 0; j < kNJ; ++j) acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x][s], bv[x][j][s], acc[x][j], 0, 0, 0);
 }
 
 __device__ __forceinline__ void wino_block(const WinoArgs& a, int& t0, int& n0, int& HWt) {
@@ -308,6 +335,29 @@ __global__ __launch_bounds__(256, kWBlocks) void wino_f23_kernel(const WinoArgs 
     for (int j = 0; j < kNJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
+#if KRRN_WINO_A2
+  // input patches two chunks ahead (their loads miss L2 more often than the L2-resident weights)
+  float d0[16], d1[16];
+  f32x4 w[kNWF];
+  sg.loadA(0, d0);
+  sg.loadB(0, w);
+  sg.loadA(1, d1);
+  for (int ck = 0; ck < sg.nchunks; ck += 2) {
+    sg.stage(d0, w, As, Bs);
+    __syncthreads();
+    sg.loadB(ck + 1, w);
+    sg.loadA(ck + 2, d0);
+    wino_mma(As, Bs, acc);
+    __syncthreads();
+    if (ck + 1 >= sg.nchunks) break;
+    sg.stage(d1, w, As, Bs);
+    __syncthreads();
+    sg.loadB(ck + 2, w);
+    sg.loadA(ck + 3, d1);
+    wino_mma(As, Bs, acc);
+    __syncthreads();
+  }
+#else
   float d[16];
   f32x4 w[kNWF];
   sg.load(0, d, w);
@@ -318,6 +368,7 @@ __global__ __launch_bounds__(256, kWBlocks) void wino_f23_kernel(const WinoArgs 
     wino_mma(As, Bs, acc);
     __syncthreads();
   }
+#endif
   wino_epilogue(a, smem, acc, t0, n0, HWt);
 }
 

@@ -35,6 +35,9 @@ from .runtime import add_conv_group, Plan, add_conv, ptr
 # as grouped launches, one per block depth (KRRN_HR_GROUP=1: 25.4 ms/step; the grouped launch
 # is bound by its slowest member and loses the cross-branch overlap of the streams)
 HR_GROUP = os.environ.get("KRRN_HR_GROUP", "0") == "1"
+# transposed convs (4 parity-class convs) as one grouped launch
+CONVT_GROUP = os.environ.get("KRRN_CONVT_GROUP", "1") == "1"
+CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
 
 BN_MOMENTUM = 0.1
 
@@ -235,6 +238,17 @@ class _Builder:
 
     def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         np_ = pad4(spec.cout)
+        if spec.kind == "convT" and CONVT_GROUP and 1 < len(spec.taps) <= 4:
+            # the parity classes write disjoint output pixels: one grouped launch (no tail per class)
+            probs = [dict(x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=x.H, Wg=x.W,
+                          in_s=1, taps=taps, wt=ptr(spec.wt[cls]), N=np_, n_store=np_, scale=ptr(spec.scale),
+                          bias=ptr(spec.bias), res=ptr(res.t) if res is not None else None,
+                          res_cs=res.cs if res is not None else 0, res_co=res.co if res is not None else 0,
+                          out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=2, osx=2, ooy=ooy,
+                          oox=oox, relu=relu, cin=spec.cin, cout=spec.cout)
+                     for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off))]
+            add_conv_group(self.plan, probs, tile=CONVT_GROUP_TILE, tag=tag + "_convT")
+            return
         for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off)):
             if spec.kind == "conv":
                 Hg, Wg, in_s, osy, osx = out.H, out.W, spec.stride, 1, 1

@@ -103,6 +103,9 @@ class KRRNPlan:
         self.normal = plan.buf((B, 3, Ho, Wo))
         plan.add("krrn_heads_select_f32", ptr(self.fx), model.xyz_outc, model.region_outc, ptr(self.fn), 3 * C,
                  ptr(self.cls), ptr(self.xyz), ptr(self.normal), B, Ho, Wo)
+        # ops[:heads_end] = backbone + heads + class select: everything after reads only xyz /
+        # normal (+ static inputs), the other PipelinedPipeline split point
+        self.heads_end = len(plan.ops)
         self.specs = [specs, bld.specs]
         self.pred_t = None
         psid = self.POSE_SID if pose_stream else 0

@@ -177,7 +177,9 @@ class PipelinedPipeline:
     math is unchanged (same kernels, per-slot buffers), only its latency is two half-steps.
     """
 
-    def __init__(self, model: KRRN, B: int, S: int, N: int, device, seed: int = 0):
+    def __init__(self, model: KRRN, B: int, S: int, N: int, device, seed: int = 0, split: str = "backbone"):
+        """split: 'backbone' (A = HRNet) or 'heads' (A = HRNet + heads + class select, B = the
+        latency-bound fusion / TBase / PnP tail)."""
         self.B, self.S, self.N, self.device = B, S, N, torch.device(device)
         self.slots = [BatchPipeline(model, B, S, N, device, parts=1, seed=2 * seed + i) for i in range(2)]
         self.stage_a: List[Tuple[Plan, dict]] = []
@@ -185,8 +187,9 @@ class PipelinedPipeline:
         for sl in self.slots:
             pt = sl.parts[0]
             kp = pt.kp
-            self.stage_a.append((_sub_plan(kp.plan, 0, kp.split), kp.env))
-            self.stage_b.append([(kp.device_perm_plan, {}), (_sub_plan(kp.plan, kp.split, len(kp.plan.ops)), kp.env),
+            cut = {"backbone": kp.split, "heads": kp.heads_end}[split]
+            self.stage_a.append((_sub_plan(kp.plan, 0, cut), kp.env))
+            self.stage_b.append([(kp.device_perm_plan, {}), (_sub_plan(kp.plan, cut, len(kp.plan.ops)), kp.env),
                                  (pt.pose, {})])
         # stage A's stream priority (KRRN_PIPE_PRIO, e.g. -1 = high): its latency-bound chain is
         # the one to keep moving while stage B's big grids occupy the CUs

@@ -56,7 +56,8 @@ def test_pipeline_matches_api_and_graph(dev, parts):
         assert torch.equal(replay[k], eager[k]), k
 
 
-def test_pipelined_matches_plain(dev):
+@pytest.mark.parametrize("split", ["backbone", "heads"])
+def test_pipelined_matches_plain(dev, split):
     """Two-stage pipeline: the batch a half-step completes equals the plain step on the same
     slot (same seed, same kernels), eager and graph-replayed."""
     from pose_estimation_amd.pipeline import PipelinedPipeline
@@ -72,7 +73,7 @@ def test_pipelined_matches_plain(dev):
         p.run()
         torch.cuda.synchronize()
         ref.append(_snap(p))
-    pp = PipelinedPipeline(m, B, S, N, dev, seed=0)
+    pp = PipelinedPipeline(m, B, S, N, dev, seed=0, split=split)
     pp.load(d)
     s0 = [sl.parts[0].kp.seed.clone() for sl in pp.slots]
     pp.run()  # B of slot 0 (+ A of slot 1)
