@@ -18,6 +18,9 @@ def _short(name: str) -> str:
     m = re.search(r"conv_gemm_f32_kernel<(\d+), (\d+), (\d+), \d+, (true|false)>", name)
     if m:
         return f"conv_gemm_f32<{m.group(1)},{m.group(2)},{m.group(3)}>" + (",nchw" if m.group(4) == "true" else "")
+    m = re.search(r"conv_group_kernel<(\d+), (\d+), (\d+), \d+>", name)
+    if m:
+        return f"conv_group<{m.group(1)},{m.group(2)},{m.group(3)}>"
     if "wino_f23_kernel" in name:
         return "wino_f23<32,32,16>"
     m = re.search(r"(\w+_kernel)", name)
