@@ -27,14 +27,24 @@
 // stores are float4 channel runs.
 // Measured and rejected (MI355X, 64 x 128 x 120 x 120): double-buffered LDS at one wave per SIMD
 // (2.24 ms vs 1.50), persistent blocks prefetching the next tile during the epilogue (1.57 ms,
-// register spills), s_setprio around the MFMA cluster (+2 %).
+// register spills), s_setprio around the MFMA cluster (+2 %), a 32-wide N tile at 3 blocks/CU
+// (1.54-1.56 ms), s-outer MFMA order / double-buffered fragments (1.51-1.52 ms), the ping-pong
+// kernel below (KRRN_WINO_V=1: 1.95 ms — staging and f32 MFMAs of the two waves on a SIMD do
+// not overlap), LDS-DMA weights (KRRN_WINO_V=2: 1.49 ms, within noise). GRBM_GUI_ACTIVE puts
+// the S=120 launch at 3.15 M cycles per XCD (clock 1.9-2.2 GHz under this load) against 1.84 M
+// cycles of MFMA issue: 58 % of the clock-adjusted f32 matrix peak.
 #include "krrn_common.h"
+
+#include <cstdlib>
 
 namespace {
 
 constexpr int kWT = 32;       // tiles per block
 #ifndef KRRN_WINO_A2
 #define KRRN_WINO_A2 0
+#endif
+#ifndef KRRN_WINO_FRAG2
+#define KRRN_WINO_FRAG2 0
 #endif
 #ifndef KRRN_WINO_EXP
 #define KRRN_WINO_EXP 0
@@ -45,7 +55,6 @@ constexpr int kWT = 32;       // tiles per block
 constexpr int kWN = KRRN_WINO_WN;  // output channels per block
 constexpr int kNJ = kWN / 32;      // 32-wide n-blocks per wave
 constexpr int kN4 = kWN / 4;       // 4-channel groups per tile
-constexpr int kNP = kWT * kN4 / 256;      // epilogue (tile, 4-channel) pairs per thread
 constexpr int kNWF = 16 * kWN * 2 / 256;  // weight float4s staged per thread per chunk
 constexpr int kWBlocks = kWN == 64 ? 2 : 3;  // blocks per CU the LDS footprint allows
 constexpr int kWC = 8;        // input channels per chunk
@@ -78,9 +87,10 @@ struct WinoArgs {
 constexpr int kSP = kWN + 4;
 static_assert(4 * 2 * kWT * kSP <= 16 * (kWT + kWN) * kWP, "epilogue staging must fit the main-loop LDS");
 
-__device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][kNJ]) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+// ADD: accumulate into what another wave group staged at the same addresses (ping-pong kernel)
+template <bool ADD = false>
+__device__ __forceinline__ void wino_epi_put(float* smem, f32x16 (&acc)[4][kNJ]) {
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
   const int fr = lane & 31;
 #pragma unroll
   for (int j = 0; j < kNJ; ++j)
@@ -88,22 +98,35 @@ __device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][kNJ
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       const float m0 = acc[0][j][r], m1 = acc[1][j][r], m2 = acc[2][j][r], m3 = acc[3][j][r];
-      smem[((wave * 2 + 0) * kWT + row) * kSP + j * 32 + fr] = m0 + m1 + m2;
-      smem[((wave * 2 + 1) * kWT + row) * kSP + j * 32 + fr] = m1 - m2 - m3;
+      float* p0 = smem + ((wave * 2 + 0) * kWT + row) * kSP + j * 32 + fr;
+      float* p1 = smem + ((wave * 2 + 1) * kWT + row) * kSP + j * 32 + fr;
+      if (ADD) {
+        *p0 += m0 + m1 + m2;
+        *p1 += m1 - m2 - m3;
+      } else {
+        *p0 = m0 + m1 + m2;
+        *p1 = m1 - m2 - m3;
+      }
     }
+}
+
+__device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][kNJ]) {
+  wino_epi_put(smem, acc);
   __syncthreads();
 }
 
+template <int NT = 256>
 __device__ __forceinline__ void wino_epi_finish(const WinoArgs& a, const float* smem, int t0, int n0, int HWt) {
+  constexpr int kNP = kWT * kN4 / NT;  // (tile, 4-channel) pairs per thread
   const int tid = threadIdx.x;
-  // geometry of this thread's 2 (tile, 4-channel) pairs and their scale / bias
+  // geometry of this thread's (tile, 4-channel) pairs and their scale / bias
   int pt[kNP], pn[kNP];
   size_t ppix[kNP][4];
   bool pok[kNP], qok[kNP][4];
   f32x4 scl[kNP], bia[kNP];
 #pragma unroll
   for (int i = 0; i < kNP; ++i) {
-    const int pr = tid + 256 * i;
+    const int pr = tid + NT * i;
     const int n4 = pr % kN4, tl = pr / kN4;
     pt[i] = tl;
     pn[i] = n0 + 4 * n4;
@@ -187,8 +210,10 @@ struct WinoStager {
   unsigned wstride;   // bytes per weight chunk
   int st, sc, cin, nchunks;
 
-  __device__ __forceinline__ WinoStager(const WinoArgs& a, int t0, int n0, int HWt) {
-    const int tid = threadIdx.x;
+  int tid;  // thread index within the staging group (0..255)
+
+  __device__ __forceinline__ WinoStager(const WinoArgs& a, int t0, int n0, int HWt, int ltid) {
+    tid = ltid;
     st = tid >> 3;
     sc = tid & 7;
     cin = a.cin;
@@ -275,7 +300,6 @@ struct WinoStager {
       As[((u * 4 + 2) * kWT + st) * kWP + sc] = t[u * 4 + 2] - t[u * 4 + 1];
       As[((u * 4 + 3) * kWT + st) * kWP + sc] = t[u * 4 + 1] - t[u * 4 + 3];
     }
-    const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < kNWF; ++i) {
       const int e = tid + 256 * i;
@@ -289,8 +313,31 @@ struct WinoStager {
 // ds_read_b128 per operand feeds 4; the s-outer order with all 12 fragments live measured equal
 // and costs 36 VGPRs).
 __device__ __forceinline__ void wino_mma(const float* As, const float* Bs, f32x16 (&acc)[4][kNJ]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
   const int fr = lane & 31, fk = (lane >> 5) * 4;
+#if KRRN_WINO_FRAG2
+  // fragments of component x+1 are read while component x's 8 MFMAs issue (no exposed
+  // ds_read latency when the SIMD's other wave is not issuing MFMAs)
+  f32x4 av[2], bv[2][kNJ];
+  auto frag = [&](int x, int slot) {
+    const int xi = 4 * wave + x;
+    av[slot] = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j)
+      bv[slot][j] = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
+  };
+  frag(0, 0);
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    if (x + 1 < 4) frag(x + 1, (x + 1) & 1);
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x & 1][s], bv[x & 1][j][s], acc[x][j], 0, 0, 0);
+  }
+  return;
+#endif
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
     const int xi = 4 * wave + x;
@@ -327,7 +374,7 @@ __global__ __launch_bounds__(256, kWBlocks) void wino_f23_kernel(const WinoArgs 
   float* Bs = smem + 16 * kWT * kWP;  // [xi][n][c]
   int t0, n0, HWt;
   wino_block(a, t0, n0, HWt);
-  const WinoStager sg(a, t0, n0, HWt);
+  const WinoStager sg(a, t0, n0, HWt, threadIdx.x);
   f32x16 acc[4][kNJ];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
@@ -372,6 +419,156 @@ __global__ __launch_bounds__(256, kWBlocks) void wino_f23_kernel(const WinoArgs 
   wino_epilogue(a, smem, acc, t0, n0, HWt);
 }
 
+// Ping-pong variant: 512 threads = two groups of 4 waves, one wave of each group per SIMD, one
+// block per CU with two LDS buffers (144 KB). Group g owns the chunks c = g (mod 2): it stages
+// chunk c into buffer c & 1 during step c-1, while the other group runs the MFMAs of chunk c-1
+// from the other buffer, and runs chunk c's MFMAs during step c. So on every SIMD one wave
+// streams MFMAs while its partner transforms / writes the next chunk (VALU and LDS issue beside
+// the matrix pipe), with ONE barrier per step; each group's loads are in flight for two steps.
+// Both groups hold partial sums over their own chunks for the whole 32 x 64 tile; the epilogue
+// adds them in the (c0, c1) staging layout and all 512 threads finish the output transform.
+constexpr int kPPBuf = 16 * (kWT + kWN) * kWP;  // floats per LDS buffer (A then B)
+static_assert(4 * 2 * kWT * kSP <= 2 * kPPBuf, "epilogue staging must fit");
+
+__global__ __launch_bounds__(512, 1) void wino_f23_pp_kernel(const WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * kPPBuf];
+  const int grp = threadIdx.x >> 8;
+  int t0, n0, HWt;
+  wino_block(a, t0, n0, HWt);
+  const WinoStager sg(a, t0, n0, HWt, threadIdx.x & 255);
+  f32x16 acc[4][kNJ];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
+  float d[16];
+  f32x4 w[kNWF];
+  const int nck = sg.nchunks;
+  sg.load(grp, d, w);
+  if (grp == 0) {  // step -1: group 0 stages chunk 0
+    sg.stage(d, w, smem, smem + 16 * kWT * kWP);
+    sg.load(2, d, w);
+  }
+  __syncthreads();
+  for (int s = 0; s < nck; ++s) {
+    if ((s & 1) == grp) {
+      const float* cur = smem + (s & 1) * kPPBuf;
+      wino_mma(cur, cur + 16 * kWT * kWP, acc);
+    } else if (s + 1 < nck) {
+      float* nxt = smem + ((s + 1) & 1) * kPPBuf;
+      sg.stage(d, w, nxt, nxt + 16 * kWT * kWP);
+      sg.load(s + 3, d, w);  // this group's next chunk (zeros past the last one)
+    }
+    __syncthreads();
+  }
+  if (grp == 1) wino_epi_put<false>(smem, acc);
+  __syncthreads();
+  if (grp == 0) wino_epi_put<true>(smem, acc);
+  __syncthreads();
+  wino_epi_finish<512>(a, smem, t0, n0, HWt);
+}
+
+// LDS-DMA variant: the transformed weights go global -> LDS with global_load_lds (16 B per
+// lane, no VGPR round trip, no ds_write), double-buffered so chunk ck+1's weights stream in
+// during chunk ck's MFMAs; only the input patches are register-staged (their transform needs
+// VALU). LDS images are unpadded with an XOR swizzle of the 16-B half of each 32-B row (bit 3 of
+// the row), which keeps every ds_read_b128 lane group and every ds_write_b32 half-wave
+// conflict-free: A [16][32][8] (16 KB) + B 2 x [16][64][8] (64 KB) = 80 KB -> 2 blocks per CU.
+// The swizzle is applied on the SOURCE address of the DMA (its LDS side is lane-linear).
+constexpr int kGA = 16 * kWT * kWC;  // floats of the A image
+constexpr int kGB = 16 * kWN * kWC;  // floats of one B image
+static_assert(4 * 2 * kWT * kSP <= kGA + 2 * kGB, "epilogue staging must fit");
+static_assert(kWN == 64, "glds B mapping assumes 64 output channels per block");
+
+__device__ __forceinline__ int wsw(int row) { return (row >> 3) & 1; }
+
+__device__ __forceinline__ void wino_mma_sw(const float* As, const float* Bs, f32x16 (&acc)[4][kNJ]) {
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
+  const int fr = lane & 31, h = lane >> 5;
+  const int ha = 4 * (h ^ wsw(fr));
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const int xi = 4 * wave + x;
+    const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWC + ha);
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) {
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWC + ha);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void wino_f23_glds_kernel(const WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[kGA + 2 * kGB];
+  float* As = smem;
+  float* Bs0 = smem + kGA;
+  int t0, n0, HWt;
+  wino_block(a, t0, n0, HWt);
+  const WinoStager sg(a, t0, n0, HWt, threadIdx.x);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // this thread's DMA slots: instruction i covers 16-B slots (4i + wave) * 64 + lane of the B
+  // image = (xi = 2i + wave/2, n = 32 (wave & 1) + lane/2, stored half lane & 1)
+  const int bn = 32 * (wave & 1) + (lane >> 1);
+  const int bh = (lane & 1) ^ wsw(bn);
+  const int gn = min(n0 + bn, a.N - 1);  // rows past N feed output channels that are never stored
+  const float* gB = a.U + ((long long)(wave >> 1) * a.N + gn) * kWC + 4 * bh;
+  const long long gstride_i = 2LL * a.N * kWC;       // floats between instruction i and i+1
+  const long long gstride_ck = 16LL * a.N * kWC;     // floats per chunk
+  auto dma_B = [&](int ck, float* Bs) {
+    const float* g = gB + ck * gstride_ck;
+#pragma unroll
+    for (int i = 0; i < kNWF; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(g + i * gstride_i),
+                                       (__attribute__((address_space(3))) void*)(Bs + ((4 * i + wave) * 64) * 4), 16,
+                                       0, 0);
+  };
+  // A write position of this thread's (tile st, channel sc) value, component xi: row xi*32+st
+  const int aw = sg.st * kWC + (sg.sc ^ (4 * wsw(sg.st)));
+  auto stageA = [&](const float (&d)[16]) {
+    float t[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
+      t[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
+      t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
+      t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      As[(u * 4 + 0) * kWT * kWC + aw] = t[u * 4 + 0] - t[u * 4 + 2];
+      As[(u * 4 + 1) * kWT * kWC + aw] = t[u * 4 + 1] + t[u * 4 + 2];
+      As[(u * 4 + 2) * kWT * kWC + aw] = t[u * 4 + 2] - t[u * 4 + 1];
+      As[(u * 4 + 3) * kWT * kWC + aw] = t[u * 4 + 1] - t[u * 4 + 3];
+    }
+  };
+  f32x16 acc[4][kNJ];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
+  float d[16];
+  dma_B(0, Bs0);
+  sg.loadA(0, d);
+  const int nck = sg.nchunks;
+  for (int ck = 0; ck < nck; ++ck) {
+    stageA(d);
+    __syncthreads();  // A(ck) written, B(ck) landed (the barrier drains the DMA)
+    if (ck + 1 < nck) {
+      dma_B(ck + 1, Bs0 + ((ck + 1) & 1) * kGB);
+      sg.loadA(ck + 1, d);
+    }
+    wino_mma_sw(As, Bs0 + (ck & 1) * kGB, acc);
+    __syncthreads();
+  }
+  wino_epilogue(a, smem, acc, t0, n0, HWt);
+}
+
 }  // namespace
 
 KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
@@ -402,6 +599,15 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   if (span >= 0x7FFF0000LL || (long long)krrn_cdiv(cin, kWC) * 16 * N * kWC * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long blocks = (long long)krrn_cdiv(a.T, kWT) * krrn_cdiv(N, kWN);
   if (blocks > 0x7fffffffLL) return KRRN_ESHAPE;
-  hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  static const int variant = [] {  // 0: register-staged, 1: ping-pong, 2: LDS-DMA weights
+    const char* e = getenv("KRRN_WINO_V");
+    return e ? atoi(e) : 0;
+  }();
+  if (variant == 1)
+    hipLaunchKernelGGL(wino_f23_pp_kernel, dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, a);
+  else if (variant == 2 && N % kWN == 0)
+    hipLaunchKernelGGL(wino_f23_glds_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }
