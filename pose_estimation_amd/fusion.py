@@ -22,7 +22,7 @@ activation.
 from __future__ import annotations
 
 import math
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, List, Optional
 
 import torch
 import torch.nn as nn
@@ -110,14 +110,15 @@ def _bn1d(bn: nn.BatchNorm1d, device):
 
 
 def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.Tensor, perms: Dict[str, torch.Tensor],
-                      hooks: Optional[Dict[str, Callable[[], None]]] = None):
+                      hooks: Optional[Dict[str, List[Callable[[dict], None]]]] = None):
     """Emit FusionNetLite.forward for P9 = [cloud | xyz_emb | nml_emb] ([B, N, 9] f32).
 
     perms: int32 device buffers 'v', 'x', 'n' ([N1] each, permutations of N), 'p1' ([N1]),
     'p2' ([N2], permutation of N1), filled before the plan runs. Returns the [B, N, 1280] buffer.
     hooks: optional callables run at named points of the emission ('level1' = after the level-1
-    branch join, 'level2' = after the level-2 kNN), e.g. to fork independent work onto a side
-    stream where the fusion leaves the chip underused.
+    branch join, 'level2' = after the level-2 kNN), each given the level buffers complete at that
+    point (feat1, feat2), e.g. to fork independent work onto a side stream where the fusion
+    leaves the chip underused.
     """
     hooks = hooks or {}
     dev = plan.device
@@ -210,16 +211,16 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
             gcn(idx1, N1, k1, off(V1, 3 * bi), N1 * 9, 3, _dn(c2.directions, dev), 128, Y2[bi],
                 _bn1d(getattr(fu, f"bn2_{br}"), dev), True, off(feat2, 128 * bi), N1 * 384, 384)
     plan.join([1, 2])
-    if "level1" in hooks:
-        hooks["level1"]()
+    for h in hooks.get("level1", []):
+        h(dict(feat1=feat1, feat2=feat2))
     # pool_2 (fusion.py:219): kNN on pool_1[..., :3] at the sampled rows
     knn(off(PV1, 0), N1 * 9, 9, N2, ptr(perms["p2"]), off(PV1, 0), N1 * 9, 9, N1, 3, 4, 1, 0, nb4b)
     plan.add("krrn_pool_max_f32", ptr(nb4b), N2, 4, off(feat2, 0), N1 * 384, 384, 384, off(FP2, 0), N2 * 384, 384, B)
     plan.add("krrn_gather_rows_f32", ptr(perms["p2"]), 0, 0, N2, off(PV1, 0), N1 * 9, 9, off(PV2, 0), N2 * 9, 9, 9, B)
     # level 2 (fusion.py:223-229): 9-D kNN, Conv_fuse_layer x2, no activation
     knn(off(PV2, 0), N2 * 9, 9, N2, ptr(None), off(PV2, 0), N2 * 9, 9, N2, 9, k2, 1, 0, idx2)
-    if "level2" in hooks:
-        hooks["level2"]()
+    for h in hooks.get("level2", []):
+        h(dict(feat1=feat1, feat2=feat2))
     plan.fork([3])
     with plan.on_stream(3):  # nearest-index to pool_2 (fusion.py:232)
         knn(off(p9, 0), N * 9, 9, N, ptr(None), off(PV2, 0), N2 * 9, 9, N2, 3, 1, 0, 1, nn2)

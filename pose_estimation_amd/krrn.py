@@ -34,8 +34,11 @@ from .config import CONFIG
 from .fusion import FEAT_SID, FusionNetLite, build_fusion_plan, level_sizes
 from .hrnet import _Builder, build_hrnet, build_hrnet_plan
 from .ops import Act, pad4
-from .posenet import PoseNet, build_tbase_plan
+from .posenet import PoseNet, build_tbase_plan, emit_tbase_level1
 from .runtime import Late, Plan, add_conv, ptr
+
+
+TBASE_EARLY = os.environ.get("KRRN_TBASE_EARLY", "1") == "1"
 
 
 class KRRNPlan:
@@ -43,6 +46,7 @@ class KRRNPlan:
 
     # side stream of the pose step when it is fused into the forward plan (pose_hook)
     POSE_SID = 6
+    TBASE_SID = 5  # TBase conv1's level-1 half (posenet.emit_tbase_level1)
     POSE_AT = os.environ.get("KRRN_POSE_AT", "level1")  # measured: level1 16.68, heads 16.80, level2 16.80 ms/step
 
     def __init__(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device, pose_hook=None,
@@ -135,17 +139,41 @@ class KRRNPlan:
             self.device_perm_plan = Plan(device)
             for sid, (k, n, m) in enumerate(self.perm_sizes):
                 self.device_perm_plan.add("krrn_randperm_i32", ptr(self.seed), sid, n, m, 1, ptr(self.perms[k]))
-            hooks = {pose_at: emit_pose} if pose_hook is not None and pose_at != "heads" else None
+            hooks = {"level1": [], "level2": []}
+            side_ids = set()  # ops the hooks emit (not FusionNetLite's)
+
+            def tracked(fn):
+                def run(fb):
+                    n0 = len(plan.ops)
+                    fn(fb)
+                    side_ids.update(id(op) for op in plan.ops[n0:])
+                return run
+
+            if pose_hook is not None and pose_at != "heads":
+                hooks[pose_at].append(tracked(lambda fb: emit_pose()))
+            # TBase conv1's level-0/1 half (P1, 0.3 ms of GEMMs) needs only feat1 / feat2: it runs on
+            # its own stream beside the level-2 GCN chain and joins before the per-point gather-add
+            tb_pre = {}
+            tb_sid = self.TBASE_SID if pose_stream else 0
+
+            def emit_tb_l1(fb):
+                plan.fork([tb_sid])
+                with plan.on_stream(tb_sid):
+                    tb_pre.update(emit_tbase_level1(model.pose.t_net, plan, B, N, N1, fb["feat1"], fb["feat2"]))
+
+            if TBASE_EARLY:
+                hooks["level1"].append(tracked(emit_tb_l1))
             f0 = len(plan.ops)
             feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms, hooks=hooks)
-            # the FusionNetLite launches (for the bench's fusion HBM roofline; pose ops excluded)
-            self.fusion_op_ids = {id(op) for op in plan.ops[f0:] if op.sid != psid and op.name != "sync"}
+            # the FusionNetLite launches (for the bench's fusion HBM roofline; hook ops excluded)
+            self.fusion_op_ids = {id(op) for op in plan.ops[f0:] if id(op) not in side_ids and op.name != "sync"}
             self.feat = feat
             fb = self.fusion_bufs
             levels = dict(fm5=fb["fm5"], feat1=fb["feat1"], feat2=fb["feat2"], nn1=fb["nn1"], nn2=fb["nn2"], N1=N1,
                           N2=N2)
             self.pred_t, self.tbase_bufs = build_tbase_plan(model.pose.t_net, plan, B, N, feat, "cls", "cloud",
-                                                            cfg.Module.POSENet.INC_R, C, levels=levels)
+                                                            cfg.Module.POSENet.INC_R, C, levels=levels,
+                                                            pre=tb_pre or None, pre_sid=tb_sid)
             plan.join([FEAT_SID])
         if pose_hook is not None:
             plan.join([psid])

@@ -12,6 +12,8 @@ conv4 + the mean over points is one reduction launch per crop.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 import torch.nn as nn
 
@@ -40,8 +42,33 @@ class PoseNet(nn.Module):
         self.t_net = TBase(cfg)
 
 
+def emit_tbase_level1(tb: TBase, plan: Plan, B: int, N: int, N1: int, feat1: torch.Tensor,
+                      feat2: torch.Tensor) -> dict:
+    """The part of TBase conv1 (by linearity, see build_tbase_plan) that needs only the level-0 /
+    level-1 features: P1 = feat1[:N1] W1[:, 512:896]^T + feat2 W1[:, 896:1280]^T, on the plan's
+    current stream. Emitted from the fusion's 'level1' hook, it runs beside the level-2 GCN chain."""
+    dev = plan.device
+    w1 = tb.conv1.weight.detach()[:, :, 0]
+    np1 = ops.pad4(1024)
+    wb = ops.make_linear(w1[:, 512:896], None, None, dev)
+    wc = ops.make_linear(w1[:, 896:1280], None, None, dev)
+    Q = plan.buf((B * N1, np1))
+    P1 = plan.buf((B * N1, np1))
+    add_conv(plan, x=ptr(feat2), x_cs=384, x_co=0, B=1, Hi=1, Wi=B * N1, cin_p=wc.cin_p, Hg=1, Wg=B * N1, in_s=1,
+             taps=[(0, 0)], wt=ptr(wc.wt[0]), N=np1, n_store=np1, scale=ptr(wc.scale), bias=ptr(wc.bias),
+             out=ptr(Q), out_cs=np1, out_co=0, Ho=1, Wo=B * N1, relu=False, cin=wc.cin, cout=wc.cout,
+             tag="tbase_gemm")
+    # feat1 rows 0..N1-1 of every crop (grid B x N1 over images of N points), + Q
+    add_conv(plan, x=ptr(feat1), x_cs=384, x_co=0, B=B, Hi=1, Wi=N, cin_p=wb.cin_p, Hg=1, Wg=N1,
+             in_s=1, taps=[(0, 0)], wt=ptr(wb.wt[0]), N=np1, n_store=np1, scale=ptr(wb.scale), bias=ptr(wb.bias),
+             res=ptr(Q), res_cs=np1, res_co=0, out=ptr(P1), out_cs=np1, out_co=0, Ho=1, Wo=N1, relu=False,
+             cin=wb.cin, cout=wb.cout, tag="tbase_gemm")
+    plan.buffers.append([wb, wc])
+    return dict(P1=P1, Q=Q)
+
+
 def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, cls_key: str, cloud_key: str,
-                     inc_r: int, num_cls: int, levels=None):
+                     inc_r: int, num_cls: int, levels=None, pre: Optional[dict] = None, pre_sid: int = 0):
     """Emit TBase + pred_t. `feat` is [B, N, inc_r]; cls ([B, 1] int64) and cloud ([B, N, 3])
     are late-bound env tensors. Returns the [B, 3] pred_t buffer.
 
@@ -50,7 +77,8 @@ def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, 
     linearity on the level rows instead of the N gathered rows: P2 = fm5 W1[:, :512]^T (N2 rows),
     P1 = feat1[:N1] W1[:, 512:896]^T + feat2 W1[:, 896:1280]^T (N1 rows; the reference indexes
     feat_1 with nearest_pool_1, so only its first N1 rows are ever read), then one gather-add
-    launch applies BN + one-hot column + ReLU per point. 29 instead of 168 GFLOP at config 2."""
+    launch applies BN + one-hot column + ReLU per point. 29 instead of 168 GFLOP at config 2.
+    `pre`: P1 already emitted by emit_tbase_level1 on stream `pre_sid` (joined here before use)."""
     dev = plan.device
     w1 = tb.conv1.weight.detach()[:, :, 0]
     spec1 = ops.make_linear(w1[:, :inc_r], tb.conv1.bias, tb.bn1, dev)
@@ -83,19 +111,14 @@ def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, 
     else:
         N1, N2 = levels["N1"], levels["N2"]
         wa = ops.make_linear(w1[:, 0:512], None, None, dev)
-        wb = ops.make_linear(w1[:, 512:896], None, None, dev)
-        wc = ops.make_linear(w1[:, 896:1280], None, None, dev)
-        keep += [wa, wb, wc]
+        keep += [wa]
         P2 = plan.buf((B * N2, np1))
-        Q = plan.buf((B * N1, np1))
-        P1 = plan.buf((B * N1, np1))
         gemm(levels["fm5"], 512, wa, P2, rows=B * N2, relu=False)
-        gemm(levels["feat2"], 384, wc, Q, rows=B * N1, relu=False)
-        # feat1 rows 0..N1-1 of every crop (grid B x N1 over images of N points), + Q
-        add_conv(plan, x=ptr(levels["feat1"]), x_cs=384, x_co=0, B=B, Hi=1, Wi=N, cin_p=wb.cin_p, Hg=1, Wg=N1,
-                 in_s=1, taps=[(0, 0)], wt=ptr(wb.wt[0]), N=np1, n_store=np1, scale=ptr(wb.scale), bias=ptr(wb.bias),
-                 res=ptr(Q), res_cs=np1, res_co=0, out=ptr(P1), out_cs=np1, out_co=0, Ho=1, Wo=N1, relu=False,
-                 cin=wb.cin, cout=wb.cout, tag="tbase_gemm")
+        if pre is None:
+            pre = emit_tbase_level1(tb, plan, B, N, N1, levels["feat1"], levels["feat2"])
+        else:
+            plan.join([pre_sid])
+        P1 = pre["P1"]
         plan.add("krrn_gather2_add_f32", ptr(levels["nn2"]), ptr(P2), N2 * np1, np1, ptr(levels["nn1"]), ptr(P1),
                  N1 * np1, np1, N, np1, ptr(spec1.scale), ptr(spec1.bias), ptr(b2), 1, ptr(h1), N * 1024, 1024, B)
     gemm(h1, 1024, spec2, h2)

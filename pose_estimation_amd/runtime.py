@@ -260,6 +260,8 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
     logical channel counts used for the algorithmic FLOP count 2*cin*cout*ntaps*M."""
     M = B * Hg * Wg
     K = cin_p * len(taps)
+    if tile is None and tag and os.environ.get(f"KRRN_TILE_{tag.upper()}"):  # tile-menu experiments
+        tile = int(os.environ[f"KRRN_TILE_{tag.upper()}"])
     tile = conv_tile(M, N, K, nchw) if tile is None else tile
     if splits is None:
         splits = 1 if nchw else conv_splits(M, N, K, tile)
