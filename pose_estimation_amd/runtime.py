@@ -228,6 +228,11 @@ TILE_SHAPES = {1: (128, 128, 16), 2: (128, 64, 16), 3: (64, 64, 16), 4: (128, 12
                6: (128, 32, 32), 7: (128, 64, 32), 8: (64, 64, 32)}
 
 
+SPLITK_TILES = int(os.environ.get("KRRN_SPLITK_TILES", "256"))  # split only launches with fewer tiles
+SPLITK_NKT = int(os.environ.get("KRRN_SPLITK_NKT", "8"))        # ... and at least this many k-tiles
+SPLITK_PER = int(os.environ.get("KRRN_SPLITK_PER", "4"))        # k-tiles per split at least
+
+
 def conv_splits(M: int, N: int, K: int, tile: int) -> int:
     """Split-K factor: layers with fewer than 256 output tiles (the 8x8 / 4x4 HRNet branches, M =
     B*64 / B*16) and a deep K get their k-tiles split across blockIdx.y until ~512 workgroups
@@ -236,9 +241,9 @@ def conv_splits(M: int, N: int, K: int, tile: int) -> int:
     cd = lambda a, b: (a + b - 1) // b  # noqa: E731
     tiles = cd(M, BM) * cd(N, BN)
     nkt = cd(K, BK)
-    if tiles >= 256 or nkt < 8 or N % 4 or os.environ.get("KRRN_SPLITK", "1") == "0":
+    if tiles >= SPLITK_TILES or nkt < SPLITK_NKT or N % 4 or os.environ.get("KRRN_SPLITK", "1") == "0":
         return 1
-    return max(1, min(cd(512, tiles), nkt // 4, 16))
+    return max(1, min(cd(512, tiles), nkt // SPLITK_PER, 16))
 
 
 CONV_KERNELS = {1: "conv_gemm_f32<128,128,16>", 2: "conv_gemm_f32<128,64,16>", 3: "conv_gemm_f32<64,64,16>",
