@@ -3,7 +3,11 @@
 A step = one pass of the hot path over one batch of synthetic LineMOD crops resident in HBM:
 HRNet-W18 + heads + class select/normalise + choose gather + FusionNetLite + TBase (pred_t)
 + batched PnP-RANSAC (R), including the device-side randomness (pool permutations, the 256-
-point PnP subset, RANSAC hypotheses). The whole step is one hipGraph replay. With --gpus N
+point PnP subset, RANSAC hypotheses). By default the step is a two-stage software pipeline over
+two batch slots (pipeline.PipelinedPipeline, split after the heads): stage A = backbone + heads of
+batch k+1 and stage B = fusion + TBase + PnP of batch k replay as two hipGraphs on two streams, so
+every step completes one whole batch (the latency-bound tail overlaps MFMA-bound convs);
+--pipeline none runs one batch end to end as one hipGraph. With --gpus N
 (torchrun, one process per GPU, RCCL) every rank runs its own batch (weak scaling) and the
 per-crop pose records are all-gathered over RCCL after every step.
 
@@ -174,9 +178,10 @@ def main():
     ap.add_argument("--micro", type=int, default=1,
                     help="micro-batches processed concurrently inside each step (pipeline.py)")
     ap.add_argument("--flat", action="store_true", help="no plan side streams inside a micro-batch")
-    ap.add_argument("--pipeline", choices=["none", "backbone", "heads"], default="none",
-                    help="two-stage pipeline (pipeline.PipelinedPipeline) split after the backbone or after the "
-                         "heads: stage A of batch k+1 runs beside stage B of batch k; none: one batch per step")
+    ap.add_argument("--pipeline", choices=["none", "backbone", "heads", "pose"], default="heads",
+                    help="two-stage pipeline (pipeline.PipelinedPipeline) split after the backbone, the heads "
+                         "(default: 16.0-16.3 vs 16.3-16.5 ms/step) or before get_pose: stage A of batch k+1 runs "
+                         "beside stage B of batch k; none: one batch per step end to end")
     args = ap.parse_args()
 
     rank, world, local = kd.init_from_env("nccl")

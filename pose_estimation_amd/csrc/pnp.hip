@@ -694,9 +694,14 @@ __global__ __launch_bounds__(kHypPerBlock) void pnp_hyp_kernel(
     int P, const float* __restrict__ xmap, const float* __restrict__ ymap, const float* __restrict__ K4,
     const double* __restrict__ extent, const double* __restrict__ lfb, const int* __restrict__ subsets, int H,
     float thr, float* __restrict__ hyp_pose, int* __restrict__ hyp_cnt) {
-  __shared__ float sobj[kPnpMaxP * 3];
-  __shared__ float simg[kPnpMaxP * 2];
-  __shared__ double sarena[kArena * kHypPerBlock];
+  // LDS sized by P (dynamic): the arena, then P object + P image points. At P = 256 this is
+  // 43.5 KB instead of 58.9 KB for kPnpMaxP: the kernel's blocks live ~1 ms beside the fusion /
+  // TBase launches, whose co-residency on those CUs the LDS footprint decides (16.42 -> 16.26
+  // ms/step measured)
+  extern __shared__ double pnp_dyn[];
+  double* sarena = pnp_dyn;
+  float* sobj = reinterpret_cast<float*>(pnp_dyn + kArena * kHypPerBlock);
+  float* simg = sobj + 3 * P;
   const int b = blockIdx.x;
   const Cam cam = {K4[4 * b + 0], K4[4 * b + 1], K4[4 * b + 2], K4[4 * b + 3]};
   load_corr(b, xyz, HW, choose, N, sel, P, xmap, ymap, extent, lfb, sobj, simg);
@@ -793,7 +798,8 @@ KRRN_API int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choo
   hipStream_t s = (hipStream_t)stream;
   float* hyp_pose = workspace;
   int* hyp_cnt = reinterpret_cast<int*>(workspace + (size_t)B * H * 12);
-  hipLaunchKernelGGL(pnp_hyp_kernel, dim3(B, krrn_cdiv(H, kHypPerBlock)), dim3(kHypPerBlock), 0, s, xyz, HW, choose,
+  const size_t hyp_lds = sizeof(double) * kArena * kHypPerBlock + sizeof(float) * 5 * (size_t)P;
+  hipLaunchKernelGGL(pnp_hyp_kernel, dim3(B, krrn_cdiv(H, kHypPerBlock)), dim3(kHypPerBlock), hyp_lds, s, xyz, HW, choose,
                      N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
   hipLaunchKernelGGL(pnp_refine_kernel, dim3(B), dim3(64), 0, s, xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent,
                      lfborder, H, thr, hyp_pose, hyp_cnt, R, t, inliers, inlier_mask);

@@ -44,7 +44,9 @@ class _Part:
 
 class BatchPipeline:
     def __init__(self, model: KRRN, B: int, S: int, N: int, device, parts: int = 1, seed: int = 0,
-                 inner_streams: bool = True, pose_stream: bool = True):
+                 inner_streams: bool = True, pose_stream: bool = True, pose_in_plan: bool = True):
+        """pose_in_plan: get_pose's launches inside the forward plan on their own stream (default),
+        or as the separate `pose` plan after it (PipelinedPipeline(split='pose'))."""
         if B % parts:
             raise ValueError(f"batch {B} not divisible into {parts} parts")
         self.B, self.S, self.N, self.device = B, S, N, torch.device(device)
@@ -63,10 +65,13 @@ class BatchPipeline:
                 res["pose"] = add_pose_ops(kp.plan, kp.xyz, kp.choose.view(b, N), b, N, xm, ym, K4, ext, lfb, kp.seed)
 
             with torch.no_grad():
-                kp = KRRNPlan(model, b, S, N, True, self.device, pose_hook=hook, pose_stream=pose_stream)
+                kp = KRRNPlan(model, b, S, N, True, self.device, pose_hook=hook if pose_in_plan else None,
+                              pose_stream=pose_stream)
             kp.seed.fill_(1000003 * (seed + 1) + 7919 * p)
-            R, t, inl, aux = res["pose"]
             pose = Plan(dev)  # after the forward plan: every reader of the seed has run
+            if not pose_in_plan:
+                res["pose"] = add_pose_ops(pose, kp.xyz, kp.choose.view(b, N), b, N, xm, ym, K4, ext, lfb, kp.seed)
+            R, t, inl, aux = res["pose"]
             pose.add("krrn_rng_advance", ptr(kp.seed))
             self.parts.append(_Part(kp, pose, xm, ym, K4, ext, lfb, R, t, inl, p * b, (p + 1) * b, aux))
         self.streams = [torch.cuda.Stream(self.device) for _ in range(parts)] if parts > 1 else []
@@ -178,17 +183,24 @@ class PipelinedPipeline:
     """
 
     def __init__(self, model: KRRN, B: int, S: int, N: int, device, seed: int = 0, split: str = "backbone"):
-        """split: 'backbone' (A = HRNet) or 'heads' (A = HRNet + heads + class select, B = the
-        latency-bound fusion / TBase / PnP tail)."""
+        """split: 'backbone' (A = HRNet), 'heads' (A = HRNet + heads + class select, B = the
+        latency-bound fusion / TBase / PnP tail) or 'pose' (A = the whole forward, B = get_pose:
+        the PnP-RANSAC of batch k, long-lived and LDS-heavy, runs beside the latency-bound
+        backbone of batch k+1 instead of the fusion / TBase tail of batch k)."""
         self.B, self.S, self.N, self.device = B, S, N, torch.device(device)
-        self.slots = [BatchPipeline(model, B, S, N, device, parts=1, seed=2 * seed + i) for i in range(2)]
-        self.stage_a: List[Tuple[Plan, dict]] = []
+        self.slots = [BatchPipeline(model, B, S, N, device, parts=1, seed=2 * seed + i, pose_in_plan=split != "pose")
+                      for i in range(2)]
+        self.stage_a: List[List[Tuple[Plan, dict]]] = []
         self.stage_b: List[List[Tuple[Plan, dict]]] = []
         for sl in self.slots:
             pt = sl.parts[0]
             kp = pt.kp
+            if split == "pose":
+                self.stage_a.append([(kp.device_perm_plan, {}), (kp.plan, kp.env)])
+                self.stage_b.append([(pt.pose, {})])
+                continue
             cut = {"backbone": kp.split, "heads": kp.heads_end}[split]
-            self.stage_a.append((_sub_plan(kp.plan, 0, cut), kp.env))
+            self.stage_a.append([(_sub_plan(kp.plan, 0, cut), kp.env)])
             self.stage_b.append([(kp.device_perm_plan, {}), (_sub_plan(kp.plan, cut, len(kp.plan.ops)), kp.env),
                                  (pt.pose, {})])
         # stage A's stream priority (KRRN_PIPE_PRIO, e.g. -1 = high): its latency-bound chain is
@@ -204,8 +216,8 @@ class PipelinedPipeline:
             s.load(data)
 
     def _run_a(self, slot: int):
-        p, env = self.stage_a[slot]
-        p.run(dict(env))
+        for p, env in self.stage_a[slot]:
+            p.run(dict(env))
 
     def _run_b(self, slot: int):
         for p, env in self.stage_b[slot]:
@@ -226,6 +238,12 @@ class PipelinedPipeline:
         run_b(b)
         main.wait_stream(self.side)
         self.h ^= 1
+
+    def reset(self):
+        """Re-run stage A of both slots (eager) from the current RNG state; the next half-step
+        completes slot 0."""
+        self._prime()
+        self.h = 0
 
     def run(self):
         if not self.primed:

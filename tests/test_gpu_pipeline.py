@@ -56,7 +56,7 @@ def test_pipeline_matches_api_and_graph(dev, parts):
         assert torch.equal(replay[k], eager[k]), k
 
 
-@pytest.mark.parametrize("split", ["backbone", "heads"])
+@pytest.mark.parametrize("split", ["backbone", "heads", "pose"])
 def test_pipelined_matches_plain(dev, split):
     """Two-stage pipeline: the batch a half-step completes equals the plain step on the same
     slot (same seed, same kernels), eager and graph-replayed."""
@@ -88,6 +88,7 @@ def test_pipelined_matches_plain(dev, split):
     pp.capture()
     for sl, s in zip(pp.slots, s0):
         sl.parts[0].kp.seed.copy_(s)
+    pp.reset()  # stage A again from the reset RNG state (split='pose': A draws the pool perms)
     pp.step()
     torch.cuda.synchronize()
     g0 = {k: v.clone() for k, v in pp.results().items()}
