@@ -684,10 +684,16 @@ __device__ void load_corr(int b, const float* xyz, int HW, const long long* choo
   }
 }
 
-constexpr int kHypPerBlock = 16;
+#ifndef KRRN_PNP_HPB
+#define KRRN_PNP_HPB 50  // measured (ms/step): 16 -> 15.98, 25 -> 15.90, 32 -> 15.83, 50 -> 15.64-15.77, 64 -> 15.75
+#endif
+constexpr int kHypPerBlock = KRRN_PNP_HPB;
 
-// Phase 1: one thread per RANSAC hypothesis; grid (B, ceil(H / 16)) spreads the 5-point EPnP
-// solves of all crops over the whole chip. Writes the f32 pose (R, t: the precision the inlier
+// Phase 1: one thread per RANSAC hypothesis; grid (B, ceil(H / kHypPerBlock)). The blocks are
+// long-lived (~1 ms of serial f64 solves) and run beside the fusion / TBase launches: 50
+// hypotheses per block (H = 100 -> 2 blocks per crop, 125 KB of LDS each, one per CU) confines
+// the kernel to ~128 CUs and leaves the rest of the chip whole, which beats spreading 448
+// quarter-wave blocks of 16 over every CU (15.7 vs 16.0 ms per step). Writes the f32 pose (R, t: the precision the inlier
 // test uses) and the inlier count of every hypothesis.
 __global__ __launch_bounds__(kHypPerBlock) void pnp_hyp_kernel(
     const float* __restrict__ xyz, int HW, const long long* __restrict__ choose, int N, const int* __restrict__ sel,
