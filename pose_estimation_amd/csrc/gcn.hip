@@ -250,35 +250,61 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
   if (p >= np) return;
   const int pi = p0 + p;
   const int SC = S * C;
-  const long long yrow = (long long)(S + 1) * C;
+  const int yrow = (S + 1) * C;  // n * yrow < 2^31 is checked on the host
   const float* yb = HAS_Y ? Y + b * (long long)n * yrow : nullptr;
   const float* dp = sdir + p * kGcnKmax * D;
   const int* nbp = snb + p * kGcnKmax;
+  constexpr int KU = KC ? KC : kGcnKmax;
+  // neighbour row offsets (floats, support block 0), hoisted out of the support loop
+  int yo[KU];
+#pragma unroll
+  for (int j = 0; j < KU; ++j) yo[j] = (KC || j < kk) ? nbp[j] * yrow + C : 0;
   for (int c = 4 * l; c < C; c += 4 * LP) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // The support loop stays rolled and, where Y is gathered, the LDS direction reads stay
+    // inside it (an opaque pointer per iteration): unrolled and hoisted into paired registers
+    // they took every VGPR (level 2, 9-D: occupancy 1, 170 -> 70 us per launch). The surface
+    // conv (no gathers, VALU-bound) keeps its hoisted directions.
+#pragma unroll 1
     for (int s = 0; s < S; ++s) {
+      const int so = s * C + c;
+      const float* dps = dp;
+      if constexpr (HAS_Y) asm volatile("" : "+v"(dps));
+      f32x4 yv[HAS_Y ? KU : 1];
+      if constexpr (HAS_Y) {
+#pragma unroll
+        for (int j = 0; j < KU; ++j)
+          if (KC || j < kk) yv[j] = *reinterpret_cast<const f32x4*>(yb + yo[j] + so);
+      }
       f32x4 w[D];
 #pragma unroll
-      for (int i = 0; i < D; ++i) w[i] = *reinterpret_cast<const f32x4*>(dn + (long long)i * SC + s * C + c);
+      for (int i = 0; i < D; ++i) w[i] = *reinterpret_cast<const f32x4*>(dn + i * SC + so);
       f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-      for (int j = 0; j < (KC ? KC : kGcnKmax); ++j) {
+      for (int j = 0; j < KU; ++j) {
         if (!KC && j >= kk) break;
-        const float* dr = dp + j * D;
-        f32x4 th = {0.f, 0.f, 0.f, 0.f};
+        const float* dr = dps + j * D;
+        f32x4 th = dr[0] * w[0];
 #pragma unroll
-        for (int i = 0; i < D; ++i) th += dr[i] * w[i];
+        for (int i = 1; i < D; ++i) th += dr[i] * w[i];
+        if constexpr (HAS_Y) {
+          // act = ReLU(theta) * support (gcn3d.py:150-156)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) th[q] = fmaxf(th[q], 0.f);
-        f32x4 val = th;
-        if constexpr (HAS_Y) val = th * *reinterpret_cast<const f32x4*>(yb + (long long)nbp[j] * yrow + C + s * C + c);
+          for (int q = 0; q < 4; ++q) th[q] = fmaxf(th[q], 0.f);
+          th *= yv[j];
+        }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], val[q]);
+        for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], th[q]);
+      }
+      if constexpr (!HAS_Y) {
+        // Conv_surface: max_k ReLU(theta) == ReLU(max_k theta) exactly (ReLU is monotone)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], 0.f);
       }
       acc += m;
     }
     f32x4 o = acc;
-    if constexpr (HAS_Y) o = *reinterpret_cast<const f32x4*>(yb + (long long)pi * yrow + c) + o;
+    if constexpr (HAS_Y) o = *reinterpret_cast<const f32x4*>(yb + pi * yrow + c) + o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (bn_s) o[q] = o[q] * bn_s[c + q] + bn_b[c + q];
@@ -300,6 +326,7 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   if (k < 1 || k > kGcnKmax || n < 1 || S < 1 || C < 1 || B < 1) return KRRN_ESHAPE;
   if ((C & 3) || (o_st & 3) || (o_bs & 3) || !krrn_aligned16(out) || !krrn_aligned16(dn)) return KRRN_EALIGN;
   if (Y && !krrn_aligned16(Y)) return KRRN_EALIGN;
+  if ((long long)n * (S + 1) * C >= (1LL << 31)) return KRRN_ESHAPE;  // 32-bit row offsets per crop
   const bool wide = C >= 512;  // LP = 128 lanes per point (see the kernel comment)
   dim3 grid(krrn_cdiv(n, wide ? kGcnThreads / 128 : kGcnThreads / 32), B);
   hipStream_t s = (hipStream_t)stream;
