@@ -252,6 +252,26 @@ int krrn_choose_points(const unsigned char* mask, int B, int S, int N, const flo
  * them (f32, sqrt(((dx*dx + dy*dy) + dz*dz)), no FMA). n <= 16384. */
 int krrn_fps_f32(const float* pts, int B, int n, int n_samples, int* out_idx, void* stream);
 
+/* BPnP forward (lib/network/dnn/BPnP.py:43-44, cv2.solvePnP(SOLVEPNP_ITERATIVE,
+ * useExtrinsicGuess=True)): Levenberg-Marquardt on sum_i ||pi(z_i; y) - x_i||^2 per crop, f64,
+ * from y_init. pts2d [B][n][2] pixels; pts3d [n][3] shared (z_per_crop = 0) or [B][n][3];
+ * K [3][3] row-major; y_init / y_out [B][6] = angle-axis (kornia convention) then t; R_init
+ * [B][9] (optional): a rotation matrix replacing y_init's angle-axis (log map), e.g. the
+ * krrn_pnp_ransac_f32 result as cv2.solvePnPRansac's rvec0 (BPnP.py:36-38); cost_out [B] final
+ * squared error (optional). At most `iters` accepted steps (stops earlier once a step is below
+ * 1e-13 relative). n >= 3. */
+int krrn_bpnp_solve_f32(const float* pts2d, const float* pts3d, int z_per_crop, const float* K, const float* y_init,
+                        const float* R_init, int B, int n, int iters, float* y_out, float* cost_out, void* stream);
+
+/* BPnP backward (lib/network/dnn/BPnP.py:53-117): implicit-function gradients of the pose P6
+ * [B][6] given grad_out [B][6]. grad_x [B][n][2]; grad_z [n][3] summed over crops (shared
+ * points) or [B][n][3] (z_per_crop); grad_K [3][3] summed over crops. workspace:
+ * B*(3n + 9) f64. Deterministic (crop-ordered sums). A singular J_fy gives NaN gradients for
+ * that crop (the reference's torch.inverse raises). */
+int krrn_bpnp_backward_f32(const float* pts2d, const float* P6, const float* pts3d, int z_per_crop, const float* K,
+                           const float* grad_out, int B, int n, float* grad_x, float* grad_z, float* grad_K,
+                           double* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

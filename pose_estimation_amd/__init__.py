@@ -11,10 +11,11 @@ Drop-in API (the reference's names):
     dataset.PoseDataset / BucketBatcher   dataset/linemod/batchdataset.py + trainer.py:521-551
     evaluate.test_epoch                   tools/trainer.py:145-250 (batched)
     fps.farthest_point_sampling           tools/script/sample_model.py:35-48
+    bpnp.BPnP / bpnp.BPnPModle            lib/network/dnn/BPnP.py (forward LM + implicit backward)
 """
 from .config import CONFIG, Cfg, make_config  # noqa: F401
 from .krrn import KRRN  # noqa: F401
-from . import dataset, fps  # noqa: F401  (register their C-ABI signatures)
+from . import bpnp, dataset, fps  # noqa: F401  (register their C-ABI signatures)
 from .loss import KRRNLoss  # noqa: F401
 from .pose import get_pose  # noqa: F401
 
