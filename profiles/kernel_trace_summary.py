@@ -24,11 +24,13 @@ def main(path, out=None):
     rows = list(csv.DictReader(open(path)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), int(r["Queue_Id"]))
                  for r in rows if "anonymous namespace" in r["Kernel_Name"]), key=lambda x: x[0])
-    # mark kernels that overlap any other kernel
+    # mark kernels that overlap any other kernel (by more than TOL ns: back-to-back kernels of
+    # one stream can show sub-microsecond timestamp overlap on a fast box)
+    TOL = 2000
     iso = []
     end_max = -1
     for i, (s, e, n, q) in enumerate(ks):
-        ov = s < end_max or (i + 1 < len(ks) and ks[i + 1][0] < e)
+        ov = s < end_max - TOL or (i + 1 < len(ks) and ks[i + 1][0] < e - TOL)
         iso.append(not ov)
         end_max = max(end_max, e)
     # serial pass = longest run of consecutive isolated kernels
