@@ -1,0 +1,33 @@
+"""krrn_resize_bilinear_f32 (HRNet fuse / final upsample, myhrnet.py:242-245, 511-516; the heads'
+UpsamplingBilinear2d, krrn.py:56, 78) against torch's F.interpolate in f32, both conventions,
+with the fused residual add + ReLU, on NHWC channel slices."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pose_estimation_amd import _lib
+from pose_estimation_amd.runtime import P, ptr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,Hi,Wi,Ho,Wo,align,fused", [
+    (128, 60, 60, 120, 120, True, False), (20, 15, 15, 30, 30, False, True), (36, 8, 8, 15, 15, False, True),
+    (144, 4, 4, 30, 30, False, False), (1024, 5, 7, 9, 13, True, True), (8, 3, 5, 40, 11, False, False)])
+def test_resize_matches_torch(dev, C, Hi, Wi, Ho, Wo, align, fused):
+    g = torch.Generator().manual_seed(C + Ho)
+    B, pad = 3, 4
+    x = torch.randn(B, C, Hi, Wi, generator=g)
+    ref = F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=align)
+    base = torch.randn(B, C, Ho, Wo, generator=g)
+    if fused:
+        ref = torch.relu(ref + base)
+    xin = torch.zeros(B, Hi, Wi, C + 2 * pad)
+    xin[..., pad:pad + C] = x.permute(0, 2, 3, 1)
+    out = torch.zeros(B, Ho, Wo, C + pad)
+    out[..., pad:] = base.permute(0, 2, 3, 1)
+    xd, od = xin.to(dev), out.to(dev)
+    add = od if fused else None
+    _lib.call("krrn_resize_bilinear_f32", ptr(xd), B, Hi, Wi, C + 2 * pad, pad, C, ptr(od), Ho, Wo, C + pad, pad,
+              ptr(add), C + pad, pad, int(align), int(fused), P(torch.cuda.current_stream().cuda_stream))
+    got = od.cpu()[..., pad:].permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
