@@ -34,7 +34,7 @@ from pose_estimation_amd import distributed as kd  # noqa: E402
 from pose_estimation_amd.config import make_config  # noqa: E402
 from pose_estimation_amd.krrn import KRRN  # noqa: E402
 from pose_estimation_amd.pipeline import BatchPipeline, PipelinedPipeline  # noqa: E402
-from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
+from pose_estimation_amd.synthetic import OBJ_DICT, init_weights, make_batch  # noqa: E402
 
 METRIC = "crops/sec at 640×480 RGB-D, 1000 sampled pts; ADD(-S) AUC vs reference"
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
@@ -171,6 +171,9 @@ def main():
     ap.add_argument("--size", type=int, default=120)
     ap.add_argument("--points", type=int, default=1000)
     ap.add_argument("--backbone", default="w18")
+    ap.add_argument("--classes", type=int, default=1,
+                    help="NUM_CLS (1 = LineMOD 'cat' config 2; 13 = LineMOD all; 5 = the ClearGrasp-sized head)")
+    ap.add_argument("--frame", default="480x640", help="source frame HxW (config 5: 960x1280)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--cpu-baseline-s", type=float, default=15.0)
@@ -189,12 +192,14 @@ def main():
     torch.cuda.set_device(dev)
     B, S, N = args.batch, args.size, args.points
 
-    cfg = make_config(num_cls=1, backbone=args.backbone)
+    C = args.classes
+    frame = tuple(int(v) for v in args.frame.split("x"))
+    cfg = make_config(num_cls=C, backbone=args.backbone)
     model = KRRN(cfg=cfg)
     init_weights(model, 0)
     model = model.to(dev).eval()
     model.perm_mode = "device"
-    data = make_batch(B, S, N, seed=1 + rank)
+    data = make_batch(B, S, N, seed=1 + rank, objlist=list(OBJ_DICT.values())[:C] if C > 1 else None, frame=frame)
     if args.pipeline == "none" or args.micro > 1:
         step = BatchPipeline(model, B, S, N, dev, parts=args.micro, seed=rank, inner_streams=not args.flat)
     else:
@@ -252,7 +257,8 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded LineMOD-shaped crops, random-init weights)",
-            "config": {"workload": f"LineMOD 'cat' batch={B}/GPU, {S}x{S} crops from 640x480 RGB-D, "
+            "config": {"workload": (f"LineMOD 'cat'" if C == 1 else f"{C}-class") +
+                                   f" batch={B}/GPU, {S}x{S} crops from {frame[1]}x{frame[0]} RGB-D, "
                                    f"HRNet-{args.backbone.upper()} + {N}-pt fusion + TBase, PnP-RANSAC (H=100) on GPU",
                        "batch_per_gpu": B, "crop": S, "points": N, "backbone": f"hrnet_{args.backbone}",
                        "parallelism": f"dp{world}" if world > 1 else "single", "graph": step.graph is not None,
