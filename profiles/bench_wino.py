@@ -8,6 +8,8 @@ dev = torch.device("cuda", 0)
 shapes = [(64, 128, 128, 120, 120), (64, 128, 128, 60, 60), (64, 272, 272, 30, 30)]
 if os.environ.get("SWEEP"): shapes = [(64, c, 128, 120, 120) for c in (32, 64, 128, 256)]
 if os.environ.get("SHAPE"): shapes = [shapes[int(os.environ["SHAPE"])]]
+if os.environ.get("SHAPES"):  # "B,cin,cout,H,W;..." e.g. the HRNet branch convs
+    shapes = [tuple(int(v) for v in t.split(",")) for t in os.environ["SHAPES"].split(";")]
 NOMIO = os.environ.get("NOMIO")
 def ev_time(fn, reps=10):
     fn(); torch.cuda.synchronize()
