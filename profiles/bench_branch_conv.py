@@ -16,6 +16,10 @@ from pose_estimation_amd.runtime import P, ptr, _iarr  # noqa: E402
 dev = torch.device("cuda", 0)
 B = int(os.environ.get("B", 64))
 shapes = [(20, 18, 30), (36, 36, 15), (72, 72, 8), (144, 144, 4)]  # (padded C, logical C, side)
+if os.environ.get("SHAPES_IDX"):  # e.g. "0,3" (PMC runs: keep the dispatch count small)
+    shapes = [shapes[int(i)] for i in os.environ["SHAPES_IDX"].split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "6,8,3,5").split(",")]
+SPLITS = [int(t) for t in os.environ.get("SPLITS", "1,2,4,8").split(",")]
 TAPS = [(dy, dx) for dy in (-1, 0, 1) for dx in (-1, 0, 1)]
 
 
@@ -45,8 +49,8 @@ for cp, c, H in shapes:
     out = torch.zeros(B, H, H, cp, device=dev)
     ws = torch.empty(16 * B * H * H * cp, device=dev)
     fl = 2.0 * B * H * H * c * c * 9
-    for tile in (6, 9, 8, 10):
-        for splits in (1, 2, 4, 8):
+    for tile in TILES:
+        for splits in SPLITS:
             def run():
                 _lib.check(L.krrn_conv2d_f32(ptr(xd), cp, 0, B, H, H, cp, H, H, 1, 9, _iarr([t[0] for t in TAPS]),
                                              _iarr([t[1] for t in TAPS]), ptr(wd), cp, cp, P(0), P(0), P(0), 1, P(0),
@@ -58,5 +62,5 @@ for cp, c, H in shapes:
                   flush=True)
     xc = x.permute(0, 3, 1, 2)[:, :c].contiguous().to(dev)
     wc = w.view(cp, 3, 3, cp).permute(0, 3, 1, 2)[:c, :c].contiguous().to(dev)
-    mm = ev_time(lambda: F.conv2d(xc, wc, padding=1))
+    mm = ev_time(lambda: F.conv2d(xc, wc, padding=1)) if not os.environ.get("NOMIO") else float("nan")
     print(f"C{c:3d} {H:2d}x{H:2d} MIOpen NCHW: {mm*1e3:7.1f} us {fl/mm/1e9:6.1f} TF", flush=True)
