@@ -87,30 +87,43 @@ def roofline_from_profile(prof, B: int):
                      **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {})}
                  for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])}
     traffic, tsrc = _pmc_traffic(dom)
-    roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
+    # achieved = what the matrix pipe issues (for Winograd F(2x2,3x3) 2.25x fewer multiplies than the
+    # direct conv it replaces), so frac <= 1 is a roofline fraction; the direct-conv-equivalent
+    # rate (SURVEY §8d's FLOP formula) is kept as `effective_tflops`
+    mp = (g["mfma"] / g["n"]) / (avg_ms * 1e-3) / 1e12 if g["mfma"] > 0 else None
+    roof = {"kernel": dom, "bound": "mfma", "achieved": round(mp, 2) if mp else None,
             "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4) if achieved else None, "traffic": traffic,
+            "frac": round(mp / PEAK_F32_MFMA_TFLOPS, 4) if mp else None, "traffic": traffic,
             "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
             "launches": g["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
-            "flops_per_launch": round(g["flops"] / g["n"]),
+            "mfma_flops_per_launch": round(g["mfma"] / g["n"]),
+            "effective_tflops": round(achieved, 2) if achieved else None,
+            "effective_flops_per_launch": round(g["flops"] / g["n"]),
             "all_conv_gemm": {"ms_per_step": round(conv_ms, 3),
                               "TFLOP/s": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2) if conv_ms else None,
                               "GFLOP_per_crop": round(conv_fl / B / 1e9, 3)},
             "all_conv": {"ms_per_step": round(allc_ms, 3), "GFLOP_per_crop": round(allc_fl / B / 1e9, 3),
-                         "TFLOP/s": round(allc_fl / (allc_ms * 1e-3) / 1e12, 2) if allc_ms else None,
-                         "frac": round(allc_fl / (allc_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4) if allc_ms else None,
+                         "effective_TFLOP/s": round(allc_fl / (allc_ms * 1e-3) / 1e12, 2) if allc_ms else None,
+                         "mfma_pipe_TFLOP/s": round(allc_mf / (allc_ms * 1e-3) / 1e12, 2) if allc_ms else None,
                          "mfma_pipe_frac": round(allc_mf / (allc_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)
                          if allc_ms else None,
-                         "note": "every conv / GEMM of the step incl. Winograd, direct-conv FLOPs (SURVEY §8d)"},
+                         "note": "every conv / GEMM of the step incl. Winograd; effective = direct-conv FLOPs "
+                                 "(SURVEY §8d), pipe = FLOPs the MFMA pipe issues"},
             "events_ms_per_step": round(total_ms, 3)}
-    if g["mfma"] and abs(g["mfma"] - g["flops"]) > 1e-6 * g["flops"]:
-        # Winograd: `achieved` counts the direct-conv FLOPs the launch replaces (SURVEY §8d's
-        # formula), so frac can exceed 1; this is what the matrix pipe actually issued
-        mp = (g["mfma"] / g["n"]) / (avg_ms * 1e-3) / 1e12
-        roof["mfma_pipe"] = {"achieved": round(mp, 2), "frac": round(mp / PEAK_F32_MFMA_TFLOPS, 4),
-                             "flops_per_launch": round(g["mfma"] / g["n"]),
-                             "note": "F(2x2,3x3) Winograd issues 2.25x fewer MFMA FLOPs than the direct conv"}
     return roof, breakdown
+
+
+def conv_subset(prof, ids):
+    """MFMA rate of the conv / GEMM launches whose op id is in `ids` (e.g. the HRNet body)."""
+    ops = [(op, ms) for op, ms in prof if id(op) in ids and op.meta.get("flops")]
+    if not ops:
+        return None
+    ms = sum(t for _, t in ops)
+    fl = sum(op.meta["flops"] for op, _ in ops)
+    mf = sum(op.meta.get("mfma_flops", op.meta["flops"]) for op, _ in ops)
+    return {"ms_per_step": round(ms, 3), "launches": len(ops), "effective_TFLOP/s": round(fl / (ms * 1e-3) / 1e12, 2),
+            "mfma_pipe_TFLOP/s": round(mf / (ms * 1e-3) / 1e12, 2),
+            "mfma_pipe_frac": round(mf / (ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)}
 
 
 def _pmc_traffic(kernel: str):
@@ -128,38 +141,144 @@ def _pmc_traffic(kernel: str):
     return round(d[kernel]["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(B: int, S: int, N: int, backbone: str, budget_s: float):
-    """The CPU oracle (PyTorch-CPU restatement + C EPnP-RANSAC) on a bounded sample."""
+def _cpu_model_name() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_config(B: int, S: int, N: int, backbone: str, warmup: int, reps: int, seed: int):
+    """crops/s of the CPU oracle (PyTorch-CPU restatement + C EPnP-RANSAC, H = 100, 1 px) on one
+    config: `warmup` untimed batches, then the median over `reps` timed batches."""
+    import statistics
     from oracle.krrn_oracle import KRRNOracle, get_pose
     from pose_estimation_amd.fusion import level_sizes
-    threads = max(1, min(16, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     m = KRRN(cfg=make_config(num_cls=1, backbone=backbone))
     sd = init_weights(m, 0)
     o = KRRNOracle(num_cls=1, backbone=backbone)
     o.load_state_dict(sd)
     o.eval()
-    bcpu = 2
-    d = make_batch(bcpu, S, N, seed=99)
+    d = make_batch(B, S, N, seed=99)
     N1, N2, _, _ = level_sizes(N, 10)
 
     def one():
         perms = [torch.randperm(N)[:N1] for _ in range(4)] + [torch.randperm(N1)[:N2]]
         pred = o(d["img_croped"], d["cloud"], d["choose"], d["cls_id"], perms=perms)
-        sel = torch.stack([torch.randperm(N)[:256] for _ in range(bcpu)])
-        subs = torch.stack([torch.stack([torch.randperm(256)[:5] for _ in range(100)]) for _ in range(bcpu)])
+        sel = torch.stack([torch.randperm(N)[:256] for _ in range(B)])
+        subs = torch.stack([torch.stack([torch.randperm(256)[:5] for _ in range(100)]) for _ in range(B)])
         get_pose(pred, d, sel, subs.int())
-    one()  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+
+    times = []
+    for i in range(warmup + reps):
+        t0 = time.perf_counter()
         one()
-        n += bcpu
         el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": round(n / el, 4), "unit": "crops/s", "cores": threads, "kind": "port",
-            "sample": f"{n} crops ({n // bcpu} batches of {bcpu}), S={S}, N={N}, HRNet-{backbone}, oracle/krrn_oracle.py "
-                      f"f32 + oracle/pnp_ref.c EPnP-RANSAC H=100, {el:.1f} s"}
+        print(f"[cpu leg] B={B} {backbone} iter {i}: {el:.2f} s", file=sys.stderr, flush=True)
+        if i >= warmup:
+            times.append(el)
+    med = statistics.median(times)
+    return {"value": round(B / med, 4), "batch": B, "backbone": f"hrnet_{backbone}", "warmup": warmup, "reps": reps,
+            "median_s_per_batch": round(med, 4)}
+
+
+def cpu_baseline(S: int, N: int, threads: int, reps2: int, warmup2: int):
+    """the CPU oracle on the GPU box's host cores, config 1 (B = 1, the reference's
+    HRNet config.yaml widths) and config 2 (B = 64, HRNet-W18), S = 120, N = 1000, crops/s as the
+    median of timed batches after warm-ups (config 1: 3 + 10; config 2: `warmup2` + `reps2`, 1 + 3
+    by default to bound the run — `--cpu-reps 10 --cpu-warmup 3` gives the full protocol)."""
+    torch.set_num_threads(threads)
+    c1 = _cpu_config(1, S, N, "lm", 3, 10, 0)
+    c2 = _cpu_config(64, S, N, "w18", warmup2, reps2, 0)
+    return {"value": c2["value"], "unit": "crops/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model_name(), "os_cpu_count": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "config1": c1, "config2": c2,
+            "sample": f"config 2 (value): B=64 'cat' S={S} N={N} HRNet-W18, median of {reps2} batches after {warmup2} "
+                      f"warm-up; config 1: B=1 HRNet config.yaml widths, median of 10 after 3; oracle/krrn_oracle.py "
+                      f"f32 + oracle/pnp_ref.c EPnP-RANSAC H=100, {threads} torch threads"}
+
+
+def cpu_leg_accuracy(dev, B: int = 64, N: int = 1000, S: int = 120, seed: int = 17):
+    """ADD(-S) AUC of the GPU pose step vs the CPU oracle's on known-pose scenes (the checker leg:
+    the oracle is only imported here and in cpu_baseline). Scenes: synthetic.make_pnp_scene, the
+    chosen pixels carry the exact normalised model coordinates of a known pose, 0.4 px noise,
+    30 % outliers at U[-20, 20] px. Both sides run the same 256-point subset and the same 100
+    RANSAC subsets (the GPU's device draws); both poses are scored with Metric against the GT
+    (half the crops as a symmetric class: ADD-S, half ADD), AUC over max_dis = 0.1 m."""
+    import numpy as np
+    from oracle import pnp as opnp
+    from pose_estimation_amd import pose
+    from pose_estimation_amd.metric import Metric, add_metric
+    from pose_estimation_amd.synthetic import make_pnp_scene
+    xyz, data, Rgt, tgt = make_pnp_scene(B, N, S, seed, outlier_frac=0.3, noise_px=0.4)
+    R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
+    torch.cuda.synchronize()
+    sel = info["sel"].cpu().long()
+    subs = info["subsets"].cpu().numpy()
+    Ro, to = [], []
+    K4 = data["intrinsic"][0].numpy()
+    for b in range(B):
+        s = sel[b]
+        pix = data["choose"][b, 0, s]
+        obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
+        img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
+        r_, t_, _, _, _ = opnp.pnp_ransac(obj, img, K4, subs[b], 1.0)
+        Ro.append(r_)
+        to.append(t_)
+    Ro = torch.from_numpy(np.stack(Ro)).float()
+    to = torch.from_numpy(np.stack(to)).float()
+    ext, lfb = data["extent"][0].numpy(), data["lfborder"][0].numpy()
+    mp = torch.from_numpy((np.random.default_rng(5).random((B, 2600, 3)) * ext + lfb).astype(np.float32))
+    target = torch.einsum("bpk,bjk->bpj", mp.double(), torch.from_numpy(Rgt)) + torch.from_numpy(tgt)[:, None]
+    target = target.float()
+    cls = (torch.arange(B) % 2).view(B, 1)
+    metric = Metric([1])
+    add_g = add_metric(R, t, mp.to(dev), target.to(dev), cls.to(dev), metric.sys).cpu().numpy()
+    add_o = add_metric(Ro.to(dev), to.to(dev), mp.to(dev), target.to(dev), cls.to(dev), metric.sys).cpu().numpy()
+    auc_g, auc_o = metric.cal_auc(list(add_g)), metric.cal_auc(list(add_o))
+    dia = float(np.linalg.norm(ext))
+    return {"auc_gpu": round(auc_g, 4), "auc_oracle": round(auc_o, 4),
+            "delta_pct": round(abs(auc_g - auc_o) / max(auc_o, 1e-9) * 100.0, 4),
+            "add_pass_gpu": float((add_g < 0.1 * dia).mean()), "add_pass_oracle": float((add_o < 0.1 * dia).mean()),
+            "max_crop_add_delta_m": float(np.abs(add_g - add_o).max()),
+            "sample": f"{B} known-pose scenes, {N} pts, 256-pt PnP subset, H=100, 0.4 px noise, 30 % outliers, "
+                      "ADD-S for half the crops; AUC max_dis 0.1 m (metric.py:38-65)"}
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N rank processes (this script, RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, one GPU each) and wait. The parent never touches the GPU, and the
+    ranks are fresh child processes (no re-exec)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
+
+
+def _dry_step(B: int, world: int, record: torch.Tensor):
+    """--dry-run stand-in for one step (no GPU): a fixed host delay for the batch, then the same
+    per-crop record all-gather the real step does (gloo)."""
+    time.sleep(0.002)
+    R = torch.eye(3).repeat(B, 1, 1)
+    t = torch.zeros(B, 3)
+    kd.pack_records(R, t, t, torch.zeros(B), out=record)
+    if world > 1:
+        kd.gather_records(record)
 
 
 def main():
@@ -176,8 +295,13 @@ def main():
     ap.add_argument("--frame", default="480x640", help="source frame HxW (config 5: 960x1280)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--cpu-baseline-s", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU leg (baseline + accuracy)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="torch threads of the CPU leg (0 = os.cpu_count())")
+    ap.add_argument("--cpu-reps", type=int, default=3, help="timed B=64 CPU batches (BASELINE.md §2 protocol: 10)")
+    ap.add_argument("--cpu-warmup", type=int, default=1, help="untimed B=64 CPU batches (protocol: 3)")
     ap.add_argument("--breakdown", default="", help="write the per-kernel breakdown JSON here")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo ranks, a host-delay step and the record all-gather (launcher rehearsal)")
     ap.add_argument("--micro", type=int, default=1,
                     help="micro-batches processed concurrently inside each step (pipeline.py)")
     ap.add_argument("--flat", action="store_true", help="no plan side streams inside a micro-batch")
@@ -187,48 +311,59 @@ def main():
                          "beside stage B of batch k; none: one batch per step end to end")
     args = ap.parse_args()
 
-    rank, world, local = kd.init_from_env("nccl")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    B, S, N = args.batch, args.size, args.points
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
 
+    rank, world, local = kd.init_from_env("gloo" if args.dry_run else "nccl")
+    B, S, N = args.batch, args.size, args.points
     C = args.classes
     frame = tuple(int(v) for v in args.frame.split("x"))
-    cfg = make_config(num_cls=C, backbone=args.backbone)
-    model = KRRN(cfg=cfg)
-    init_weights(model, 0)
-    model = model.to(dev).eval()
-    model.perm_mode = "device"
-    data = make_batch(B, S, N, seed=1 + rank, objlist=list(OBJ_DICT.values())[:C] if C > 1 else None, frame=frame)
-    if args.pipeline == "none" or args.micro > 1:
-        step = BatchPipeline(model, B, S, N, dev, parts=args.micro, seed=rank, inner_streams=not args.flat)
+    step = None
+    if args.dry_run:
+        dev = torch.device("cpu")
+        record = torch.zeros((B, kd.RECORD), dtype=torch.float32)
+        one_step = lambda: _dry_step(B, world, record)  # noqa: E731
+        sync = lambda: None  # noqa: E731
     else:
-        step = PipelinedPipeline(model, B, S, N, dev, seed=rank, split=args.pipeline)
-    step.load(data)
-    record = torch.zeros((B, kd.RECORD), dtype=torch.float32, device=dev)
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        cfg = make_config(num_cls=C, backbone=args.backbone)
+        model = KRRN(cfg=cfg)
+        init_weights(model, 0)
+        model = model.to(dev).eval()
+        model.perm_mode = "device"
+        data = make_batch(B, S, N, seed=1 + rank, objlist=list(OBJ_DICT.values())[:C] if C > 1 else None, frame=frame)
+        if args.pipeline == "none" or args.micro > 1:
+            step = BatchPipeline(model, B, S, N, dev, parts=args.micro, seed=rank, inner_streams=not args.flat)
+        else:
+            step = PipelinedPipeline(model, B, S, N, dev, seed=rank, split=args.pipeline)
+        step.load(data)
+        record = torch.zeros((B, kd.RECORD), dtype=torch.float32, device=dev)
+        step.run()  # eager warm-up (compiles nothing; touches every buffer)
+        torch.cuda.synchronize()
+        if not args.no_graph:
+            step.capture()
 
-    step.run()  # eager warm-up (compiles nothing; touches every buffer)
-    torch.cuda.synchronize()
-    if not args.no_graph:
-        step.capture()
-
-    def one_step():
-        step.step()
-        if world > 1:
-            r = step.results()  # the batch this step completed
-            kd.pack_records(r["R"], r["t"], r["pred_t"], r["inliers"], out=record)
-            kd.gather_records(record)
+        def one_step():
+            step.step()
+            if world > 1:
+                r = step.results()  # the batch this step completed
+                kd.pack_records(r["R"], r["t"], r["pred_t"], r["inliers"], out=record)
+                kd.gather_records(record)
+        sync = torch.cuda.synchronize
 
     for _ in range(args.warmup):
         one_step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -240,34 +375,50 @@ def main():
     value = world * B * args.steps / el
 
     roof, breakdown = None, None
-    if rank == 0 and not args.no_profile:
+    extra = {}
+    if rank == 0 and step is not None and not args.no_profile:
         step.profile()  # warm the eager path once
         prof = step.profile()
         roof, breakdown = roofline_from_profile(prof, B)
-        fids = set().union(*(getattr(pt.kp, "fusion_op_ids", set()) for pt in step.parts))
+        parts = step.parts
+        fids = set().union(*(getattr(pt.kp, "fusion_op_ids", set()) for pt in parts))
         roof["fusion"] = fusion_roofline(prof, fids, B, N)
+        bids = set().union(*({id(op) for op in pt.kp.plan.ops[:pt.kp.split]} for pt in parts))
+        roof["hrnet_body"] = conv_subset(prof, bids)
+        extra = {"fusion_hbm_frac": (roof["fusion"] or {}).get("frac"),
+                 "conv_mfma_frac": roof["all_conv"]["mfma_pipe_frac"],
+                 "hrnet_conv_mfma_frac": (roof["hrnet_body"] or {}).get("mfma_pipe_frac")}
         if args.breakdown:
             with open(args.breakdown, "w") as f:
                 json.dump({"roofline": roof, "kernels": breakdown}, f, indent=1)
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline_s > 0:
-        cpu = cpu_baseline(2, S, N, args.backbone, args.cpu_baseline_s)
+    cpu, acc = None, None
+    if rank == 0 and world == 1 and step is not None and not args.no_cpu:
+        acc = cpu_leg_accuracy(dev)
+        threads = args.cpu_threads or (os.cpu_count() or 1)
+        cpu = cpu_baseline(S, N, threads, args.cpu_reps, args.cpu_warmup)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded LineMOD-shaped crops, random-init weights)",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "dry run (no GPU)" if args.dry_run else
+                    "synthetic (seeded LineMOD-shaped crops, random-init weights)",
             "config": {"workload": (f"LineMOD 'cat'" if C == 1 else f"{C}-class") +
                                    f" batch={B}/GPU, {S}x{S} crops from {frame[1]}x{frame[0]} RGB-D, "
                                    f"HRNet-{args.backbone.upper()} + {N}-pt fusion + TBase, PnP-RANSAC (H=100) on GPU",
-                       "batch_per_gpu": B, "crop": S, "points": N, "backbone": f"hrnet_{args.backbone}",
-                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": step.graph is not None,
+                       "batch_per_gpu": B, "global_batch": B * world, "crop": S, "points": N,
+                       "backbone": f"hrnet_{args.backbone}",
+                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "graph": step is not None and step.graph is not None,
                        "micro_batches": args.micro,
-                       "pipeline": "none" if isinstance(step, BatchPipeline) else
+                       "pipeline": "none" if isinstance(step, BatchPipeline) or step is None else
                        f"2-stage split after the {args.pipeline} (stage A of batch k+1 beside stage B of batch k; "
                        "one batch completes per step)"},
-            "roofline": roof, "cpu_baseline": cpu,
+            **extra,
+            "roofline": roof, "cpu_baseline": cpu, "accuracy": acc,
         }
+        if args.dry_run:
+            line["dry_run"] = True
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -212,6 +212,10 @@ int krrn_map_losses_ws(int B, int HW, long long* n_doubles);
 int krrn_map_losses_f32(const float* xyz, const float* xyz_gt, const float* nml, const float* nml_gt,
                         const float* region, int R, const long long* region_gt, const float* mask, int M,
                         const long long* mask_gt, int B, int HW, double* ws, double* out, void* stream);
+/* Per-crop form, read from the ws a preceding krrn_map_losses_f32(B, HW) filled (same stream):
+ * out_crop f64 [B][8] = crop b's four losses then its four valid counts. The reference's test
+ * loop runs batch size 1 and adds each crop's own losses to its object (tools/trainer.py:180-182). */
+int krrn_map_losses_crop_f32(const double* ws, int B, int HW, double* out_crop, void* stream);
 
 /* PoseLoss (lib/network/loss.py:19-42) with the GT rotation and the predicted translation as
  * KRRNLoss calls it (:66-67): pred = model_points [B][P][3] @ target_r[b]^T + pred_t[b]; for
@@ -222,6 +226,15 @@ int krrn_pose_loss_ws(int B, int P, long long* n_doubles);
 int krrn_pose_loss_f32(const float* target_r, const float* pred_t, const float* target, const float* model_points,
                        const long long* cls_id, const int* sym, int nsym, int B, int P, double* ws, double* out,
                        void* stream);
+
+/* ADD(-S) per crop (Metric.cal_adds_cuda, lib/utils/metric.py:17-35, called by Trainer.cal_dis,
+ * tools/trainer.py:370-381): pred = model_points [B][P][3] @ pred_r[b]^T + pred_t[b]; out f64 [B]
+ * = mean_i |pred_i - target_i| (ADD), or for cls_id[b] in sym[0..nsym) mean over targets i of
+ * min over preds j |pred_j - target_i| (ADD-S, exact direct-difference norms). ws: the same
+ * size as krrn_pose_loss_ws(B, P). Deterministic. */
+int krrn_add_metric_f32(const float* pred_r, const float* pred_t, const float* model_points, const float* target,
+                        const long long* cls_id, const int* sym, int nsym, int B, int P, double* ws, double* out,
+                        void* stream);
 
 /* On-GPU input construction, replacing PoseDataset._load_data's per-sample numpy
  * work (dataset/linemod/batchdataset.py:603-771) for B crops of one snapped square size S.

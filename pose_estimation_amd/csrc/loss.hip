@@ -127,6 +127,28 @@ __global__ __launch_bounds__(kLossThreads) void map_losses_final_kernel(const do
   }
 }
 
+// per-crop means: block b sums crop b's partial records [nbx][8] in index order -> out[b][0..3]
+// = sum / count (0 without a valid pixel), out[b][4..7] = counts. trainer.py:180-182 adds each
+// crop's own loss (batch size 1) to its object's running sums.
+__global__ __launch_bounds__(kLossThreads) void map_losses_crop_kernel(const double* __restrict__ part, int nbx,
+                                                                     double* __restrict__ out) {
+  __shared__ double red[kLossThreads / 64];
+  __shared__ double tot[8];
+  const double* pb = part + (size_t)blockIdx.x * nbx * 8;
+  for (int k = 0; k < 8; ++k) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < nbx; i += kLossThreads) v += pb[(size_t)i * 8 + k];
+    const double t = block_sum(v, red);
+    if (threadIdx.x == 0) tot[k] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const double c = tot[4 + threadIdx.x];
+    out[(size_t)blockIdx.x * 8 + threadIdx.x] = c > 0.0 ? tot[threadIdx.x] / c : 0.0;
+    out[(size_t)blockIdx.x * 8 + 4 + threadIdx.x] = c;
+  }
+}
+
 // PoseLoss: grid (ceil(P / 256), B); targets of crop b staged through LDS in tiles for the
 // nearest-point search of symmetric classes
 constexpr int kPoseTile = 2048;
@@ -200,6 +222,80 @@ __global__ __launch_bounds__(kLossThreads) void pose_loss_final_kernel(const dou
   if (threadIdx.x == 0) out[0] = t / (double)B;
 }
 
+// ADD / ADD-S per crop (Metric.cal_adds_cuda, lib/utils/metric.py:17-35, as Trainer.cal_dis calls
+// it, tools/trainer.py:370-381): pred = model_points @ R^T + t; ADD = mean_i |pred_i - target_i|;
+// for a symmetric class ADD-S = mean over targets i of min over preds j |pred_j - target_i| (the
+// reference's [N, N, 3] broadcast, norm over dim 2, min over dim 1). grid (ceil(P / 256), B):
+// one target per thread, the crop's predicted points rebuilt into LDS tile by tile; the min is
+// taken over exact direct-difference squared norms (no expanded-distance shortcut), then sqrt.
+__global__ __launch_bounds__(kLossThreads) void add_metric_kernel(const float* __restrict__ R, const float* __restrict__ t,
+                                                                  const float* __restrict__ mp,
+                                                                  const float* __restrict__ target,
+                                                                  const long long* __restrict__ cls,
+                                                                  const int* __restrict__ sym, int nsym, int P,
+                                                                  double* __restrict__ part) {
+  __shared__ float pl[kPoseTile * 3];
+  __shared__ double red[kLossThreads / 64];
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * kLossThreads + threadIdx.x;
+  const float* Rb = R + (size_t)b * 9;
+  const float* tb = t + (size_t)b * 3;
+  const float* mb = mp + (size_t)b * P * 3;
+  const float* tg = target + (size_t)b * P * 3;
+  bool is_sym = false;
+  const long long c = cls[b];
+  for (int k = 0; k < nsym; ++k) is_sym |= (long long)sym[k] == c;
+  float qx = 0.f, qy = 0.f, qz = 0.f;
+  if (i < P) {
+    qx = tg[(size_t)i * 3];
+    qy = tg[(size_t)i * 3 + 1];
+    qz = tg[(size_t)i * 3 + 2];
+  }
+  double v = 0.0;
+  if (!is_sym) {  // block-uniform
+    if (i < P) {
+      const float* m = mb + (size_t)i * 3;
+      const float px = m[0] * Rb[0] + m[1] * Rb[1] + m[2] * Rb[2] + tb[0];
+      const float py = m[0] * Rb[3] + m[1] * Rb[4] + m[2] * Rb[5] + tb[1];
+      const float pz = m[0] * Rb[6] + m[1] * Rb[7] + m[2] * Rb[8] + tb[2];
+      const float dx = px - qx, dy = py - qy, dz = pz - qz;
+      v = sqrtf(dx * dx + dy * dy + dz * dz);
+    }
+  } else {
+    float best = INFINITY;
+    for (int j0 = 0; j0 < P; j0 += kPoseTile) {
+      const int nj = min(kPoseTile, P - j0);
+      __syncthreads();
+      for (int e = threadIdx.x; e < nj; e += kLossThreads) {
+        const float* m = mb + (size_t)(j0 + e) * 3;
+        pl[3 * e] = m[0] * Rb[0] + m[1] * Rb[1] + m[2] * Rb[2] + tb[0];
+        pl[3 * e + 1] = m[0] * Rb[3] + m[1] * Rb[4] + m[2] * Rb[5] + tb[1];
+        pl[3 * e + 2] = m[0] * Rb[6] + m[1] * Rb[7] + m[2] * Rb[8] + tb[2];
+      }
+      __syncthreads();
+      if (i < P) {
+        for (int j = 0; j < nj; ++j) {
+          const float dx = pl[3 * j] - qx, dy = pl[3 * j + 1] - qy, dz = pl[3 * j + 2] - qz;
+          best = fminf(best, dx * dx + dy * dy + dz * dz);
+        }
+      }
+    }
+    if (i < P) v = sqrtf(best);
+  }
+  const double s = block_sum(v, red);
+  if (threadIdx.x == 0) part[(size_t)b * gridDim.x + blockIdx.x] = s;
+}
+
+// per crop: fixed-order sum of its nblk partials / P
+__global__ __launch_bounds__(kLossThreads) void add_metric_final_kernel(const double* __restrict__ part, int nblk,
+                                                                       int B, int P, double* __restrict__ out) {
+  const int b = blockIdx.x * kLossThreads + threadIdx.x;
+  if (b >= B) return;
+  double s = 0.0;
+  for (int k = 0; k < nblk; ++k) s += part[(size_t)b * nblk + k];
+  out[b] = s / (double)P;
+}
+
 }  // namespace
 
 KRRN_API int krrn_map_losses_ws(int B, int HW, long long* n_doubles) {
@@ -224,6 +320,14 @@ KRRN_API int krrn_map_losses_f32(const float* xyz, const float* xyz_gt, const fl
   return krrn_launch_status();
 }
 
+KRRN_API int krrn_map_losses_crop_f32(const double* ws, int B, int HW, double* out_crop, void* stream) {
+  if (!ws || !out_crop) return KRRN_EARG;
+  if (B < 1 || HW < 1) return KRRN_ESHAPE;
+  hipLaunchKernelGGL(map_losses_crop_kernel, dim3(B), dim3(kLossThreads), 0, (hipStream_t)stream, ws,
+                     krrn_cdiv(HW, kLossPixPerBlock), out_crop);
+  return krrn_launch_status();
+}
+
 KRRN_API int krrn_pose_loss_ws(int B, int P, long long* n_doubles) {
   if (!n_doubles) return KRRN_EARG;
   if (B < 1 || P < 1) return KRRN_ESHAPE;
@@ -242,5 +346,20 @@ KRRN_API int krrn_pose_loss_f32(const float* target_r, const float* pred_t, cons
   hipLaunchKernelGGL(pose_loss_kernel, dim3(nbx, B), dim3(kLossThreads), 0, s, target_r, pred_t, target, model_points,
                      cls_id, sym, nsym, P, ws);
   hipLaunchKernelGGL(pose_loss_final_kernel, dim3(1), dim3(kLossThreads), 0, s, ws, nbx, B, P, out);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_add_metric_f32(const float* pred_r, const float* pred_t, const float* model_points,
+                                 const float* target, const long long* cls_id, const int* sym, int nsym, int B, int P,
+                                 double* ws, double* out, void* stream) {
+  if (!pred_r || !pred_t || !model_points || !target || !cls_id || !ws || !out || (nsym > 0 && !sym))
+    return KRRN_EARG;
+  if (B < 1 || P < 1 || B > 65535 || nsym < 0) return KRRN_ESHAPE;
+  const int nbx = krrn_cdiv(P, kLossThreads);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(add_metric_kernel, dim3(nbx, B), dim3(kLossThreads), 0, s, pred_r, pred_t, model_points, target,
+                     cls_id, sym, nsym, P, ws);
+  hipLaunchKernelGGL(add_metric_final_kernel, dim3(krrn_cdiv(B, kLossThreads)), dim3(kLossThreads), 0, s, ws, nbx, B,
+                     P, out);
   return krrn_launch_status();
 }

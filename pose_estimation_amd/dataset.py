@@ -8,20 +8,35 @@ normalisation, mask, random `choose`, back-projected cloud. Here the box snap st
 a whole bucket of equal-size crops at once in two HIP launches (krrn_crop_inputs_u8,
 krrn_choose_points). The frames live on the GPU.
 
-No LineMOD data ships with the reference and there is no network, so `root=None` (the default)
+`root` = a LineMOD tree in the reference's layout (Linemod_preprocessed): per object
+`data/XX/{test,train}.txt` (image ids), `data/XX/gt.yml` (cam_R_m2c, cam_t_m2c in mm, obj_bb;
+for benchvise the entry with obj_id 2, batchdataset.py:152-153, 229-240), `data/XX/rgb/NNNN.png`,
+`data/XX/depth/NNNN.png` (uint16 mm), `data/XX/mask/NNNN.png` (mask_label = channel 0 == 255;
+mode 'eval': `segnet_results/XX_label/NNNN_label.png` == 255, :197-244), and
+`models/obj_XX.ply` (ascii PLY vertices / 1000, ply_vtx :841-852; 2600 random model points at
+test time, :700-704). Only the crop sizes (from gt.yml's boxes) are read up front; each batch
+reads and decodes its frames (a thread pool) and stages them to the GPU. Not read: the per-frame
+GT-map pickles (xyz / normal / region, :202-212) — they feed only the logged loss terms and the
+`mask_obj` factor of the point mask, so here the mask is mask_label * mask_depth (documented
+deviation) and the loss keys are absent.
+
+`root=None` (the default; no LineMOD data ships with the reference and there is no network)
 serves seeded synthetic 640x480 RGB-D frames built like the real ones (an object mask inside a
 YOLO-like detection box whose snapped sizes follow the LineMOD test histogram, a depth plane
 with an object bump, LineMOD intrinsics and models_info extents, a GT pose and model points).
 
     ds = PoseDataset("test", 1000, False, None, 0.0, 8, cls_type="all")
+    ds = PoseDataset("test", 1000, False, "/data/Linemod_preprocessed", 0.0, 8, cls_type="cat")
     for S, idx in BucketBatcher(ds, bs=64):      # f3: equal-S batches (trainer.py:521-551)
         data = ds.batch(idx, device)             # the eval keys of :730-771, on the GPU
 """
 from __future__ import annotations
 
 import ctypes
+import os
 import random
 from collections import OrderedDict
+from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -189,16 +204,94 @@ def build_inputs(frames: Dict[str, torch.Tensor], frame_idx: Sequence[int], boxe
             "point_mask": mask.view(B, 1, S, S), "mask_count": cnt}
 
 
+def ply_vtx(path: str) -> np.ndarray:
+    """Vertices of an ascii PLY (batchdataset.py:841-852: the element count on the 4th line, x y z
+    the first three fields of each vertex line), f32 [n, 3] in the file's units."""
+    with open(path) as f:
+        if f.readline().strip() != "ply":
+            raise ValueError(f"{path}: not a PLY file")
+        n = None
+        fmt = None
+        while True:
+            line = f.readline()
+            if not line:
+                raise ValueError(f"{path}: no end_header")
+            tok = line.split()
+            if tok[:1] == ["format"]:
+                fmt = tok[1]
+            if tok[:2] == ["element", "vertex"]:
+                n = int(tok[2])
+            if line.strip() == "end_header":
+                break
+        if fmt != "ascii" or n is None:
+            raise ValueError(f"{path}: only ascii PLY vertex lists are read (format {fmt})")
+        return np.array([np.float32(f.readline().split()[:3]) for _ in range(n)], dtype=np.float32)
+
+
+def _read_lines(p: str) -> List[str]:
+    with open(p) as f:
+        return [ln.strip() for ln in f if ln.strip()]
+
+
+class _LinemodTree:
+    """Index of a LineMOD tree (module doc): one entry per (object, image id) of the split, its GT
+    pose and detection box from gt.yml; frames are read on demand."""
+
+    def __init__(self, root: str, mode: str, objlist: Sequence[int], n_model_pts: int, seed: int):
+        import yaml
+        self.root, self.mode = root, mode
+        self.items: List[Dict[str, object]] = []
+        self.model_points: Dict[int, np.ndarray] = {}
+        rng = np.random.default_rng(seed)
+        split = "train.txt" if mode == "train" else "test.txt"
+        for obj in objlist:
+            croot = os.path.join(root, "data", f"{obj:02d}")
+            with open(os.path.join(croot, "gt.yml")) as f:
+                meta = yaml.safe_load(f)
+            for im in _read_lines(os.path.join(croot, split)):
+                entries = meta[int(im)]
+                e = entries[0]
+                if obj == 2:  # benchvise frames list several objects (batchdataset.py:230-234)
+                    e = next((m for m in entries if int(m["obj_id"]) == 2), e)
+                self.items.append({"obj": obj, "im": int(im), "R": np.resize(np.array(e["cam_R_m2c"], np.float64), (3, 3)),
+                                   "t": np.array(e["cam_t_m2c"], np.float64) / 1000.0,
+                                   "bbox": [float(v) for v in e["obj_bb"]]})
+            pts = ply_vtx(os.path.join(root, "models", f"obj_{obj:02d}.ply")) / 1000.0
+            if len(pts) > n_model_pts:  # random deletion down to num_pt_mesh_large (:700-704)
+                keep = np.sort(rng.choice(len(pts), n_model_pts, replace=False))
+                pts = pts[keep]
+            self.model_points[obj] = pts.astype(np.float32)
+
+    def read(self, i: int):
+        it = self.items[i]
+        croot = os.path.join(self.root, "data", f"{int(it['obj']):02d}")
+        im = int(it["im"])
+        from PIL import Image
+        with Image.open(os.path.join(croot, "rgb", f"{im:04d}.png")) as ri:
+            rgb = np.array(ri)[:, :, :3]
+        with Image.open(os.path.join(croot, "depth", f"{im:04d}.png")) as di:
+            # depth / cam_scale (f64) then float32, as _load_data's depth_choosed (:714-716)
+            depth = (np.asarray(di).astype(np.float64) / 1000.0).astype(np.float32)
+        if self.mode == "eval":
+            lp = os.path.join(self.root, "segnet_results", f"{int(it['obj']):02d}_label", f"{im:04d}_label.png")
+        else:
+            lp = os.path.join(croot, "mask", f"{im:04d}.png")
+        with Image.open(lp) as li:
+            label = np.array(li)
+        ml = (label[:, :, 0] if label.ndim == 3 else label) == 255
+        return rgb, depth, ml.astype(np.uint8)
+
+
 class PoseDataset(torch.utils.data.Dataset):
-    """The reference's constructor signature (batchdataset.py:34); root=None serves synthetic
-    frames (module doc). Eval only: add_noise / noise_trans / num_kps are accepted and unused."""
+    """The reference's constructor signature (batchdataset.py:34); `root` = a LineMOD tree, or
+    None for synthetic frames (module doc). Eval only: add_noise / noise_trans / num_kps are
+    accepted and unused."""
 
     def __init__(self, mode: str = "test", num_point: int = 1000, add_noise: bool = False, root: Optional[str] = None,
                  noise_trans: float = 0.0, num_kps: int = 8, cls_type: Optional[str] = None, cfg=CONFIG,
-                 num_frames: int = 256, seed: int = 0, sizes: Optional[Sequence[int]] = None):
-        if root is not None:
-            raise NotImplementedError("no LineMOD data ships with the reference; root=None serves synthetic frames")
-        self.mode, self.num_point, self.cfg = mode, num_point, cfg
+                 num_frames: int = 256, seed: int = 0, sizes: Optional[Sequence[int]] = None,
+                 n_model_pts: int = 2600, io_threads: int = 8):
+        self.mode, self.num_point, self.cfg, self.root = mode, num_point, cfg, root
         if cls_type in (None, "all"):
             self.objlist = list(LM_OBJLIST)
         else:
@@ -206,8 +299,15 @@ class PoseDataset(torch.utils.data.Dataset):
         self.sym_obj = [i for i in SYM_OBJ if i < len(self.objlist)] if len(self.objlist) > 1 else []
         info = models_info()
         self.diameter = [info[o]["diameter"] / 1000.0 for o in self.objlist]
-        self.frames_np = synthetic_frames(num_frames, seed, self.objlist, sizes=sizes)
-        self.boxes = [get_square_bbox([float(v) for v in bb]) for bb in self.frames_np["bbox"]]
+        self.io_threads = io_threads
+        if root is not None:
+            self.tree = _LinemodTree(root, mode, self.objlist, n_model_pts, seed)
+            self.frames_np = None
+            self.boxes = [get_square_bbox(it["bbox"]) for it in self.tree.items]
+        else:
+            self.tree = None
+            self.frames_np = synthetic_frames(num_frames, seed, self.objlist, sizes=sizes)
+            self.boxes = [get_square_bbox([float(v) for v in bb]) for bb in self.frames_np["bbox"]]
         self._dev_frames: Dict[str, Dict[str, torch.Tensor]] = {}
         self._seed: Dict[str, torch.Tensor] = {}
         self._calls = 0
@@ -219,39 +319,70 @@ class PoseDataset(torch.utils.data.Dataset):
         rmin, rmax, _, _ = self.boxes[i]
         return rmax - rmin
 
+    def _seed_for(self, device) -> torch.Tensor:
+        key = str(device)
+        if key not in self._seed:
+            self._seed[key] = torch.tensor([int(np.random.SeedSequence(len(self)).generate_state(1)[0])],
+                                           dtype=torch.int64, device=device)
+        return self._seed[key]
+
     def frames(self, device) -> Dict[str, torch.Tensor]:
+        """Synthetic frames, resident on `device` (all of them: 2.4 MB per 640x480 frame)."""
         key = str(device)
         if key not in self._dev_frames:
             self._dev_frames[key] = {k: torch.from_numpy(self.frames_np[k]).to(device)
                                      for k in ("rgb", "depth", "mask_label")}
-            self._seed[key] = torch.tensor([int(np.random.SeedSequence(len(self)).generate_state(1)[0])],
-                                           dtype=torch.int64, device=device)
         return self._dev_frames[key]
+
+    def _read_frames(self, idx: Sequence[int], device) -> Dict[str, torch.Tensor]:
+        """Decode the batch's frames from the tree (thread pool) and stage them on `device`."""
+        with ThreadPoolExecutor(max_workers=max(1, min(self.io_threads, len(idx)))) as ex:
+            fr = list(ex.map(self.tree.read, idx))
+        return {"rgb": torch.from_numpy(np.stack([f[0] for f in fr])).to(device, non_blocking=True),
+                "depth": torch.from_numpy(np.stack([f[1] for f in fr])).to(device, non_blocking=True),
+                "mask_label": torch.from_numpy(np.stack([f[2] for f in fr])).to(device, non_blocking=True)}
+
+    def _meta(self, i: int):
+        """(obj id, R [3,3] f64, t [3] f64, model points [P,3] f32) of crop i."""
+        if self.tree is not None:
+            it = self.tree.items[i]
+            obj = int(it["obj"])
+            return obj, it["R"], it["t"], self.tree.model_points[obj]
+        f = self.frames_np
+        return (int(f["obj_id"][i]), f["target_r"][i].astype(np.float64), f["target_t"][i].astype(np.float64),
+                f["model_points"][i])
 
     def batch(self, indices: Sequence[int], device) -> Dict[str, torch.Tensor]:
         """The eval keys of batchdataset.py:730-771 for `indices` (one crop size), collated."""
         device = torch.device(device)
-        fr = self.frames(device)
-        fnp = self.frames_np
         idx = list(indices)
+        if self.tree is not None:
+            fr = self._read_frames(idx, device)
+            fidx = list(range(len(idx)))
+        else:
+            fr = self.frames(device)
+            fidx = idx
         K4 = torch.tensor([[LM_K[0, 0], LM_K[1, 1], LM_K[0, 2], LM_K[1, 2]]] * len(idx), dtype=torch.float32)
         self._calls += 1
-        out = build_inputs(fr, idx, [self.boxes[i] for i in idx], self.num_point, K4, self._seed[str(device)],
+        out = build_inputs(fr, fidx, [self.boxes[i] for i in idx], self.num_point, K4, self._seed_for(device),
                            stream_id=self._calls)
         info = models_info()
-        ext = [np.array(info[fnp["obj_id"][i]]["size"]) / 1000.0 for i in idx]
-        lfb = [np.array(info[fnp["obj_id"][i]]["min"]) / 1000.0 for i in idx]
-        R = torch.from_numpy(fnp["target_r"][idx])
-        t = torch.from_numpy(fnp["target_t"][idx])
-        mp = torch.from_numpy(fnp["model_points"][idx])
+        metas = [self._meta(i) for i in idx]
+        ext = [np.array(info[m[0]]["size"]) / 1000.0 for m in metas]
+        lfb = [np.array(info[m[0]]["min"]) / 1000.0 for m in metas]
+        R64 = torch.from_numpy(np.stack([m[1] for m in metas]))
+        t64 = torch.from_numpy(np.stack([m[2] for m in metas]))
+        npt = min(len(m[3]) for m in metas)
+        mp = torch.from_numpy(np.stack([m[3][:npt] for m in metas]))
         host = {
-            "cls_id": torch.tensor([[self.objlist.index(int(fnp["obj_id"][i]))] for i in idx], dtype=torch.int64),
+            "cls_id": torch.tensor([[self.objlist.index(m[0])] for m in metas], dtype=torch.int64),
             "intrinsic": K4,
             "extent": torch.from_numpy(np.stack(ext)),
             "lfborder": torch.from_numpy(np.stack(lfb)),
             "bbox": torch.tensor([[b[0], b[1], b[2], b[3]] for b in (self.boxes[i] for i in idx)], dtype=torch.float32),
-            "target_r": R, "target_t": t, "model_points": mp,
-            "target": (mp @ R.transpose(1, 2) + t[:, None]).float(),
+            "target_r": R64.float(), "target_t": t64.float(), "model_points": mp,
+            # model_points @ target_r.T + target_t in f64, then float32 (batchdataset.py:706, 765)
+            "target": (mp.double() @ R64.transpose(1, 2) + t64[:, None]).float(),
         }
         out.update({k: v.to(device) for k, v in host.items()})
         return out

@@ -1,24 +1,39 @@
-"""Batched eval epoch: Trainer.test_epoch (tools/trainer.py:145-250) over
-size-bucketed batches instead of one crop per step.
+"""Batched, sharded eval epoch: Trainer.test_epoch
+(tools/trainer.py:145-250) over size-bucketed batches instead of one crop per step, split across
+ranks.
 
 Per batch of equal-size crops (BucketBatcher): the GPU-built inputs (PoseDataset.batch), one
-KRRN forward, the eval-time KRRNLoss map terms when the batch carries GT maps, get_pose (PnP-
-RANSAC, the "base" R / t) and the TBase translation (the "reg" / "final" t). The per-object
-bookkeeping keeps the reference's result keys and thresholds (ADD(-S) < 0.1 d, 5 deg, 5 cm), and
+KRRN forward, the eval-time KRRNLoss map terms per crop when the batch carries GT maps
+(krrn_map_losses_crop_f32: the reference's batch-size-1 loop adds each crop's own losses,
+trainer.py:180-182), get_pose (PnP-RANSAC, the "base" R / t), the TBase translation (the "reg" /
+"final" t) and ADD(-S) / rotation / translation errors for the whole batch in one launch
+(metric.cal_dis_batch). Each crop leaves one f64 record (REC fields below).
+
+Multi-GPU (one process per GPU): every rank evaluates its own contiguous slice of every S bucket
+(distributed.bucket_shard), the per-crop records are all-gathered (RCCL all_gather_into_tensor;
+every rank knows every shard's size from the crop sizes, so records are padded to the largest
+shard, no size exchange), and every rank folds them in global crop order — so the result dict,
+sums included, is bit-identical for any world size. One all_reduce of the success counts checks
+the gathered table against the ranks' own tallies.
+
+The per-object bookkeeping keeps the reference's result keys and thresholds (ADD(-S) < 0.1 d,
+5 deg, 5 cm); test_dis sums final ADD(-S) with opt_pose and base ADD(-S) without (:232-247);
 the ADD(-S) AUC of Metric.cal_auc (metric.py:38-65) is reported per object and overall.
 """
 from __future__ import annotations
 
 import copy
-from collections import defaultdict
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
+import torch.distributed as dist
 
-from .dataset import BucketBatcher, PoseDataset
+from . import distributed as kd
+from .dataset import PoseDataset
 from .krrn import KRRN
-from .loss import KRRNLoss
-from .metric import Metric, cal_dis
+from .loss import map_losses
+from .metric import Metric, cal_dis_batch
 from .pose import get_pose
 
 ROT_THR_DEG = 5.0     # trainer.py:156
@@ -27,56 +42,141 @@ _KEYS = ("all_num", "obj_num", "succ_base_rt", "dis_base_rt", "succ_base_r", "di
          "dis_base_t", "succ_reg_rt", "dis_reg_rt", "succ_reg_r", "dis_reg_r", "succ_reg_t", "dis_reg_t",
          "succ_final_rt", "dis_final_rt", "succ_final_r", "dis_final_r", "succ_final_t", "dis_final_t",
          "dis_mask", "dis_normal", "dis_xyz")
+# per-crop record (f64)
+REC = ("crop", "cls", "add_b", "r_b", "t_b", "add_f", "r_f", "t_f", "l_xyz", "l_mask", "l_normal", "valid")
+_R = {k: i for i, k in enumerate(REC)}
+
+
+def _batches(buckets: Dict[int, List[int]], bs: int):
+    for S in sorted(buckets):
+        idx = buckets[S]
+        for lo in range(0, len(idx), bs):
+            yield S, idx[lo:lo + bs]
+
+
+@torch.no_grad()
+def eval_records(model: KRRN, dataset: PoseDataset, indices: Dict[int, List[int]], bs: int, device,
+                 opt_pose: bool = True, with_loss: bool = True) -> torch.Tensor:
+    """Run the eval path over {S: [crop indices]} in batches of <= bs; returns f64 [n, len(REC)]
+    (rows in the order evaluated)."""
+    metric = Metric(dataset.sym_obj)
+    rows = []
+    for S, idx in _batches(indices, bs):
+        data = dataset.batch(idx, device)
+        pred = model(data["img_croped"], data["cloud"], data["choose"], data["cls_id"], opt_pose=opt_pose)
+        B = len(idx)
+        rec = np.zeros((B, len(REC)), dtype=np.float64)
+        rec[:, _R["crop"]] = idx
+        rec[:, _R["cls"]] = data["cls_id"].reshape(B).cpu().numpy()
+        rec[:, _R["valid"]] = 1.0
+        if with_loss and "xyz" in data and "multi_cls_mask" in data:
+            lc = map_losses(pred, data, per_crop=True).cpu().numpy()  # [B, 8]: xyz, normal, region, mask, counts
+            rec[:, _R["l_xyz"]] = lc[:, 0]
+            rec[:, _R["l_normal"]] = lc[:, 1]
+            rec[:, _R["l_mask"]] = lc[:, 3]
+        base_r, base_t = get_pose(pred, data)
+        a, r, t = cal_dis_batch(metric, base_r, base_t, data)
+        rec[:, _R["add_b"]], rec[:, _R["r_b"]], rec[:, _R["t_b"]] = a, r, t
+        if opt_pose:
+            # reg = final = (PnP R, TBase t) (trainer.py:198-201)
+            a, r, t = cal_dis_batch(metric, base_r, pred["pred_t"], data)
+            rec[:, _R["add_f"]], rec[:, _R["r_f"]], rec[:, _R["t_f"]] = a, r, t
+        rows.append(rec)
+    if not rows:
+        return torch.zeros((0, len(REC)), dtype=torch.float64)
+    return torch.from_numpy(np.concatenate(rows))
+
+
+def fold_records(records: torch.Tensor, objlist: Sequence[int], diameter: Sequence[float], opt_pose: bool,
+                 metric: Metric) -> Dict[str, object]:
+    """The reference's per-object bookkeeping (trainer.py:165-250) over per-crop records, in global
+    crop order (independent of how crops were batched or sharded)."""
+    rec = records[records[:, _R["valid"]] > 0]
+    rec = rec[torch.argsort(rec[:, _R["crop"]], stable=True)].numpy()
+    result = {k: {o: 0.0 for o in objlist} for k in _KEYS}
+    adds: Dict[int, List[float]] = {}
+    test_dis = 0.0
+    for row in rec:
+        cls = int(row[_R["cls"]])
+        obj = objlist[cls]
+        dia = diameter[cls]
+        result["all_num"][obj] += 1
+        result["obj_num"][obj] += 1
+        ab, rb, tb = row[_R["add_b"]], row[_R["r_b"]], row[_R["t_b"]]
+        result["dis_base_rt"][obj] += ab
+        result["dis_base_r"][obj] += rb
+        result["dis_base_t"][obj] += tb
+        result["succ_base_rt"][obj] += ab < 0.1 * dia
+        result["succ_base_r"][obj] += rb < ROT_THR_DEG
+        result["succ_base_t"][obj] += tb < TRANS_THR_M
+        result["dis_xyz"][obj] += row[_R["l_xyz"]]
+        result["dis_mask"][obj] += row[_R["l_mask"]]
+        result["dis_normal"][obj] += row[_R["l_normal"]]
+        if opt_pose:
+            af, rf, tf = row[_R["add_f"]], row[_R["r_f"]], row[_R["t_f"]]
+            for k in ("reg", "final"):
+                result[f"dis_{k}_rt"][obj] += af
+                result[f"dis_{k}_r"][obj] += rf
+                result[f"dis_{k}_t"][obj] += tf
+                result[f"succ_{k}_rt"][obj] += af < 0.1 * dia
+                result[f"succ_{k}_r"][obj] += rf < ROT_THR_DEG
+                result[f"succ_{k}_t"][obj] += tf < TRANS_THR_M
+            test_dis += af
+            adds.setdefault(obj, []).append(float(af))
+        else:
+            test_dis += ab
+            adds.setdefault(obj, []).append(float(ab))
+    out = copy.copy(result)
+    out["test_count"] = int(len(rec))
+    out["test_dis"] = test_dis / max(len(rec), 1)
+    out["auc"] = {o: metric.cal_auc(v) for o, v in adds.items()}
+    out["auc_all"] = metric.cal_auc([a for v in adds.values() for a in v]) if adds else 0.0
+    return out
+
+
+def gather_epoch_records(local: torch.Tensor, shard_sizes: Sequence[int], device, group=None) -> torch.Tensor:
+    """All-gather every rank's [n_r, len(REC)] records (padded to max(shard_sizes) rows, pad rows
+    have valid = 0) -> all ranks' records, rank-major."""
+    world = len(shard_sizes)
+    if world == 1:
+        return local
+    m = max(shard_sizes)
+    pad = torch.zeros((max(m, 1), len(REC)), dtype=torch.float64)
+    pad[:local.shape[0]] = local
+    backend = dist.get_backend(group)
+    buf = pad.to(device) if backend == "nccl" else pad
+    out = kd.gather_records(buf, group=group)
+    return out.cpu()
 
 
 @torch.no_grad()
 def test_epoch(model: KRRN, dataset: PoseDataset, bs: int = 64, device=None, opt_pose: bool = True,
-               criterion: Optional[KRRNLoss] = None) -> Dict[str, object]:
+               criterion=None, world: Optional[int] = None, rank: Optional[int] = None,
+               group=None) -> Dict[str, object]:
+    """Trainer.test_epoch over `dataset`. world/rank default to the initialised process group
+    (1/0 without one). `criterion` enables the per-crop map-loss terms (dis_xyz / dis_mask /
+    dis_normal) when the batches carry GT maps; the reference always evaluates it (:167)."""
     device = torch.device(device) if device is not None else next(model.parameters()).device
-    objlist = dataset.objlist
+    if world is None:
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+    sizes = [dataset.crop_size(i) for i in range(len(dataset))]
+    mine = kd.bucket_shard(sizes, world, rank)
+    local = eval_records(model, dataset, mine, bs, device, opt_pose=opt_pose, with_loss=criterion is not None)
+    shard_sizes = [sum(len(v) for v in kd.bucket_shard(sizes, world, r).values()) for r in range(world)]
+    allrec = gather_epoch_records(local, shard_sizes, device, group) if world > 1 else local
     metric = Metric(dataset.sym_obj)
-    result = {k: {o: 0.0 for o in objlist} for k in _KEYS}
-    adds = defaultdict(list)
-    count, test_dis = 0, 0.0
-    for S, idx in BucketBatcher(dataset, bs):
-        data = dataset.batch(idx, device)
-        pred = model(data["img_croped"], data["cloud"], data["choose"], data["cls_id"], opt_pose=opt_pose)
-        losses = criterion(pred, data, opt_pose=False) if criterion is not None and "xyz" in data else None
-        base_r, base_t = get_pose(pred, data)
-        B = len(idx)
-        for b in range(B):
-            cls = int(data["cls_id"][b])
-            obj = objlist[cls]
-            dia = dataset.diameter[cls]
-            result["all_num"][obj] += 1
-            result["obj_num"][obj] += 1
-            add, r, t = cal_dis(metric, base_r, base_t, data, b)
-            result["dis_base_rt"][obj] += add
-            result["dis_base_r"][obj] += r
-            result["dis_base_t"][obj] += t
-            result["succ_base_rt"][obj] += add < 0.1 * dia
-            result["succ_base_r"][obj] += r < ROT_THR_DEG
-            result["succ_base_t"][obj] += t < TRANS_THR_M
-            if losses is not None:
-                result["dis_xyz"][obj] += float(losses["loss_xyz"])
-                result["dis_mask"][obj] += float(losses["loss_mask"])
-                result["dis_normal"][obj] += float(losses["loss_normal"])
-            if opt_pose:
-                # reg = (PnP R, TBase t) = final (trainer.py:198-201)
-                add, r, t = cal_dis(metric, base_r, pred["pred_t"], data, b)
-                for k in ("reg", "final"):
-                    result[f"dis_{k}_rt"][obj] += add
-                    result[f"dis_{k}_r"][obj] += r
-                    result[f"dis_{k}_t"][obj] += t
-                    result[f"succ_{k}_rt"][obj] += add < 0.1 * dia
-                    result[f"succ_{k}_r"][obj] += r < ROT_THR_DEG
-                    result[f"succ_{k}_t"][obj] += t < TRANS_THR_M
-                test_dis += add
-            adds[obj].append(add)
-            count += 1
-    out = copy.copy(result)
-    out["test_count"] = count
-    out["test_dis"] = test_dis / max(count, 1)
-    out["auc"] = {o: metric.cal_auc(v) for o, v in adds.items()}
-    out["auc_all"] = metric.cal_auc([a for v in adds.values() for a in v])
+    out = fold_records(allrec, dataset.objlist, dataset.diameter, opt_pose, metric)
+    if world > 1:
+        # the ranks' own crop / success tallies, summed, must equal the gathered table's
+        key = "add_f" if opt_pose else "add_b"
+        dia = torch.tensor([dataset.diameter[int(c)] for c in local[:, _R["cls"]]], dtype=torch.float64)
+        mine_t = torch.tensor([float(local.shape[0]), float((local[:, _R[key]] < 0.1 * dia).sum())],
+                              dtype=torch.float64)
+        t = mine_t.to(device) if dist.get_backend(group) == "nccl" else mine_t
+        dist.all_reduce(t, group=group)
+        tot = t.cpu()
+        succ_key = "succ_final_rt" if opt_pose else "succ_base_rt"
+        assert int(tot[0]) == out["test_count"], (tot, out["test_count"])
+        assert int(tot[1]) == int(sum(out[succ_key].values())), (tot, out[succ_key])
     return out

@@ -17,12 +17,18 @@ Randomness (the five torch.randperm draws of the Pool_layers, gcn3d.py:239):
                      shared by the batch — reference semantics;
   perm_mode='device' counter-based draws on the GPU (krrn_randperm_i32), for graph replay;
   perms=[...]        explicit permutations (parity tests).
-Outputs are views of plan-owned buffers that the next forward of the same shape overwrites
-(CUDA-graph static-output semantics); clone them to keep them.
+Outputs are fresh tensors, like the reference's (krrn.py:155-165). `model.return_views = True`
+returns views of the plan-owned buffers instead (no copy; the next forward of the same shape
+overwrites them — CUDA-graph static-output semantics).
+
+Plans are cached per (B, S, N, opt_pose) in an LRU bounded by bytes (`plan_budget_bytes`,
+default 48 GiB or KRRN_PLAN_BUDGET_GB; a plan's workspaces are ~5 GB at B=64, S=120, N=1000 and
+grow ~ B*S^2): an eval over many crop-size buckets keeps the most recently used plans only.
 """
 from __future__ import annotations
 
 import os
+from collections import OrderedDict
 
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -178,6 +184,7 @@ class KRRNPlan:
         if pose_hook is not None:
             plan.join([psid])
         self.env = {"cls": self.cls, "cloud": self.cloud}
+        self.nbytes = plan_bytes(plan) + plan_bytes(getattr(self, "device_perm_plan", None))
 
     def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):
         B, Cx, Ho, Wo = out.shape
@@ -224,6 +231,16 @@ class KRRNPlan:
         }
 
 
+def plan_bytes(plan) -> int:
+    """Device bytes a Plan's workspaces hold (its keep-alive tensors)."""
+    if plan is None:
+        return 0
+    return sum(t.numel() * t.element_size() for t in plan.buffers if isinstance(t, torch.Tensor))
+
+
+PLAN_BUDGET = int(float(os.environ.get("KRRN_PLAN_BUDGET_GB", "48")) * (1 << 30))
+
+
 class KRRN(nn.Module):
     def __init__(self, num_cls: int = 1, cfg=CONFIG):
         super().__init__()
@@ -263,7 +280,9 @@ class KRRN(nn.Module):
         self.nml_final = nn.Conv2d(nml_channels, nml_out, kernel_size=(1, 1))
         self.fusion = FusionNetLite(cfg)
         self.pose = PoseNet(cfg)
-        self._plans: Dict[Tuple, KRRNPlan] = {}
+        self._plans: "OrderedDict[Tuple, KRRNPlan]" = OrderedDict()
+        self.plan_budget_bytes = PLAN_BUDGET
+        self.return_views = False
         self.perm_mode = "host"
 
     # plans fold the weights: any weight change invalidates them
@@ -281,14 +300,33 @@ class KRRN(nn.Module):
     def get_plan(self, B: int, S: int, N: int, opt_pose: bool = True) -> KRRNPlan:
         key = (B, S, N, bool(opt_pose))
         p = self._plans.get(key)
-        if p is None:
-            dev = next(self.parameters()).device
-            if dev.type != "cuda":
-                raise RuntimeError("KRRN runs on the MI355X HIP path only: call .cuda() first")
-            with torch.no_grad():
-                p = KRRNPlan(self, B, S, N, opt_pose, dev)
-            self._plans[key] = p
+        if p is not None:
+            self._plans.move_to_end(key)
+            return p
+        dev = next(self.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("KRRN runs on the MI355X HIP path only: call .cuda() first")
+        # make room first (least recently used plans go; their workspaces return to torch's
+        # caching allocator and are reused by the new plan)
+        while self._plans and self.plans_bytes() + self._estimate(B, S, N) > self.plan_budget_bytes:
+            self._plans.popitem(last=False)
+        with torch.no_grad():
+            p = KRRNPlan(self, B, S, N, opt_pose, dev)
+        self._plans[key] = p
         return p
+
+    def plans_bytes(self) -> int:
+        return sum(p.nbytes for p in self._plans.values())
+
+    def _estimate(self, B: int, S: int, N: int) -> int:
+        """Workspace bytes of a new plan, extrapolated from a cached one (~ B*S^2 for the maps plus
+        ~ B*N for the points); 0 when nothing is cached yet."""
+        best = None
+        for (b, s, n, _), p in self._plans.items():
+            r = (B * S * S) / max(1, b * s * s)
+            est = int(p.nbytes * r)
+            best = est if best is None else max(best, est)
+        return best or 0
 
     @torch.no_grad()
     def forward(self, x, p_emb, choose, cls, region_point=None, opt_pose=True, perms=None):
@@ -300,4 +338,7 @@ class KRRN(nn.Module):
         p.load_inputs(x, p_emb, choose, cls)
         p.set_perms(perms, self.perm_mode)
         p.run()
-        return p.outputs(self)
+        out = p.outputs(self)
+        if self.return_views:
+            return out
+        return {k: (v.clone() if v is not None else None) for k, v in out.items()}

@@ -27,6 +27,7 @@ _I = ctypes.c_int
 _L = ctypes.c_longlong
 _lib.register("krrn_map_losses_ws", [_I, _I, P])
 _lib.register("krrn_map_losses_f32", [P, P, P, P, P, _I, P, P, _I, P, _I, _I, P, P, P])
+_lib.register("krrn_map_losses_crop_f32", [P, _I, _I, P, P])
 _lib.register("krrn_pose_loss_ws", [_I, _I, P])
 _lib.register("krrn_pose_loss_f32", [P, P, P, P, P, P, _I, _I, _I, P, P, P])
 
@@ -49,8 +50,10 @@ def _i64(t: Optional[torch.Tensor], dev) -> Optional[torch.Tensor]:
     return None if t is None else t.to(device=dev, dtype=torch.int64).contiguous()
 
 
-def map_losses(pred: Dict[str, torch.Tensor], gt: Dict[str, torch.Tensor]) -> torch.Tensor:
-    """f64 [8]: l1(xyz), 1-cos(normal), CE(region), CE(mask), then the four valid-pixel counts."""
+def map_losses(pred: Dict[str, torch.Tensor], gt: Dict[str, torch.Tensor], per_crop: bool = False) -> torch.Tensor:
+    """f64 [8]: l1(xyz), 1-cos(normal), CE(region), CE(mask), then the four valid-pixel counts
+    (valid pixels pooled over the batch). per_crop=True: f64 [B, 8], each crop's own terms — what
+    the reference's batch-size-1 test loop accumulates per object (trainer.py:180-182)."""
     xyz = pred["xyz"]
     dev = xyz.device
     if not xyz.is_cuda:
@@ -65,6 +68,10 @@ def map_losses(pred: Dict[str, torch.Tensor], gt: Dict[str, torch.Tensor]) -> to
     _lib.call("krrn_map_losses_f32", ptr(_f32(xyz, dev)), ptr(_f32(gt["xyz"], dev)), ptr(_f32(pred["normal"], dev)),
               ptr(_f32(gt["normal"], dev)), ptr(region), region.shape[1], ptr(region_gt), ptr(mask), mask.shape[1],
               ptr(mask_gt), B, HW, ptr(ws), ptr(out), _stream(dev))
+    if per_crop:
+        oc = torch.empty((B, 8), dtype=torch.float64, device=dev)
+        _lib.call("krrn_map_losses_crop_f32", ptr(ws), B, HW, ptr(oc), _stream(dev))
+        return oc
     return out
 
 

@@ -1,9 +1,10 @@
 """Pose-accuracy harness: Metric (lib/utils/metric.py:13-113) and Trainer.cal_dis
 (tools/trainer.py:370-381) — the ADD(-S) / AUC half of BASELINE.json's metric.
 
-ADD-S's nearest-prediction search (the reference broadcasts an [N, N, 3] tensor, metric.py:27-30)
-runs on the HIP kNN kernel (krrn_knn_f32, mode 1, k = 1) when the points are on the GPU; the
-distances of the selected pairs, means, quaternion angle and AUC are scalar bookkeeping.
+ADD / ADD-S (the reference broadcasts an [N, N, 3] tensor for ADD-S, metric.py:27-31) run for a
+whole batch of crops in one HIP launch (krrn_add_metric_f32: model points transformed on the
+fly, exact direct-difference norms, min over predictions per target); quaternion angle,
+translation error and AUC are vectorised host bookkeeping.
 """
 from __future__ import annotations
 
@@ -12,20 +13,31 @@ from typing import List, Sequence, Tuple
 import numpy as np
 import torch
 
+import ctypes
+
 from . import _lib
 from .runtime import P, ptr
 
+_I = ctypes.c_int
+_lib.register("krrn_add_metric_f32", [P, P, P, P, P, P, _I, _I, _I, P, P, P])
 
-def _nearest_gpu(query: torch.Tensor, cand: torch.Tensor) -> torch.Tensor:
-    """For each query row, the index of its nearest candidate (f32 expanded distance)."""
-    q = query.contiguous().float()
-    c = cand.contiguous().float()
-    nq, nc = q.shape[0], c.shape[0]
-    out = torch.empty((1, nq, 1), dtype=torch.int32, device=q.device)
-    st = P(torch.cuda.current_stream(q.device).cuda_stream)
-    _lib.check(_lib.lib().krrn_knn_f32(ptr(q), nq * 3, 3, nq, ptr(None), ptr(c), nc * 3, 3, nc, 3, 1, 0, 1, 1,
-                                       ptr(out), st), "krrn_knn_f32")
-    return out.view(nq).long()
+
+def add_metric(pred_r: torch.Tensor, pred_t: torch.Tensor, model_points: torch.Tensor, target: torch.Tensor,
+               cls_id: torch.Tensor, sym: Sequence[int]) -> torch.Tensor:
+    """f64 [B]: ADD, or ADD-S for crops whose cls_id is in `sym`, of pred = mp @ R^T + t against
+    target (metric.py:17-35 per crop), one krrn_add_metric_f32 launch for the batch."""
+    dev = pred_t.device
+    if dev.type != "cuda":
+        raise RuntimeError("add_metric runs on the HIP path only (GPU tensors)")
+    B, Pn = model_points.shape[0], model_points.shape[1]
+    f = lambda x: x.to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
+    symt = torch.tensor(list(sym) or [0], dtype=torch.int32, device=dev)
+    ws = torch.empty((B * ((Pn + 255) // 256),), dtype=torch.float64, device=dev)
+    out = torch.empty((B,), dtype=torch.float64, device=dev)
+    _lib.call("krrn_add_metric_f32", ptr(f(pred_r).reshape(B, 9)), ptr(f(pred_t).reshape(B, 3)), ptr(f(model_points)),
+              ptr(f(target)), ptr(cls_id.to(device=dev, dtype=torch.int64).reshape(B).contiguous()), ptr(symt),
+              len(sym), B, Pn, ptr(ws), ptr(out), P(torch.cuda.current_stream(dev).cuda_stream))
+    return out
 
 
 def rotation_matrix_to_quaternion(R: torch.Tensor) -> torch.Tensor:
@@ -56,17 +68,15 @@ class Metric:
         self.sys = list(sym)
 
     def cal_adds_cuda(self, pred: torch.Tensor, target: torch.Tensor, idx: int) -> Tuple[float, float]:
+        """metric.py:17-35 for one crop's already-transformed points (identity pose through the
+        batched kernel)."""
         assert pred.dim() == target.dim() == 2
-        add = float(torch.linalg.norm(pred - target, dim=1).mean())
-        if idx in self.sys:
-            if pred.is_cuda:
-                nn = _nearest_gpu(target, pred)
-                adds = float(torch.linalg.norm(target - pred[nn], dim=1).mean())
-            else:  # host bookkeeping path for CPU tensors (harness only)
-                d = torch.cdist(target.double(), pred.double())
-                adds = float(d.min(dim=1)[0].mean())
-            return adds, adds
-        return add, add
+        dev = pred.device
+        eye = torch.eye(3, device=dev).view(1, 3, 3)
+        zero = torch.zeros((1, 3), device=dev)
+        v = float(add_metric(eye, zero, pred.unsqueeze(0), target.unsqueeze(0),
+                             torch.tensor([int(idx)], device=dev), self.sys)[0])
+        return v, v
 
     def cal_auc(self, add_dis: List[float], max_dis: float = 0.1) -> float:
         D = np.array(add_dis, dtype=np.float64)
@@ -100,6 +110,25 @@ class Metric:
     @staticmethod
     def translation_distance(t1, t2):
         return torch.norm(t1 - t2, dim=-1)
+
+
+def cal_dis_batch(metric: Metric, pred_r: torch.Tensor, pred_t: torch.Tensor, datas):
+    """Trainer.cal_dis (trainer.py:370-381) for every crop of a batch: (ADD(-S) [B], rotation error
+    deg [B], translation error m [B]) as f64 numpy arrays."""
+    dev = pred_t.device
+    B = pred_t.shape[0]
+    add = add_metric(pred_r, pred_t.reshape(B, 3), datas["model_points"], datas["target"], datas["cls_id"],
+                     metric.sys).cpu().numpy()
+    R = pred_r.detach().float().cpu().reshape(B, 3, 3)
+    Rt = datas["target_r"].detach().float().cpu().reshape(B, 3, 3)
+    q1 = torch.nn.functional.normalize(rotation_matrix_to_quaternion(R), p=2.0, dim=-1, eps=1e-12)
+    q2 = torch.nn.functional.normalize(rotation_matrix_to_quaternion(Rt), p=2.0, dim=-1, eps=1e-12)
+    dot = (q1 * q2).sum(-1)
+    eps = 1e-7
+    r = (2 * torch.acos(torch.clamp(dot.abs(), -1.0 + eps, 1.0 - eps)) / torch.pi * 180.0).numpy()
+    t = torch.norm(pred_t.detach().float().cpu().reshape(B, 3) - datas["target_t"].detach().float().cpu().reshape(B, 3),
+                   dim=-1).double().numpy()
+    return add, r, t
 
 
 def cal_dis(metric: Metric, pred_r: torch.Tensor, pred_t: torch.Tensor, datas, b: int = 0):

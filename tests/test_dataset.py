@@ -58,3 +58,45 @@ def test_bucket_batcher_covers_every_crop_once():
         seen += idx
     assert sorted(seen) == list(range(len(sizes)))
     assert len(bb) == len(list(bb))
+
+
+def test_linemod_tree_index_and_frames(tmp_path):
+    """PoseDataset(root=...) on a LineMOD-layout tree: the split lists, gt.yml poses (benchvise's
+    obj_id-2 entry), boxes snapped by get_square_bbox, frames decoded as the reference reads them
+    (rgb[:, :, :3], depth / 1000 in f64 -> f32, mask channel 0 == 255; 'eval' reads segnet labels)
+    and 2600 model points from the ascii PLY (/ 1000)."""
+    import numpy as np
+    from linemod_tree import write_tree
+    from pose_estimation_amd.dataset import PoseDataset, get_square_bbox, ply_vtx
+
+    from pose_estimation_amd.config import LM_OBJLIST
+    w = write_tree(str(tmp_path), objs=LM_OBJLIST, per_obj=2)
+    for mode in ("test", "eval"):
+        ds = PoseDataset(mode, 500, False, str(tmp_path), 0.0, 8, cls_type="all")
+        assert len(ds) == 26 and ds.sym_obj == [7, 8]
+        assert ds.boxes == [get_square_bbox(it["bbox"]) for it in ds.tree.items]
+        for i, it in enumerate(ds.tree.items):
+            ref = w[(it["obj"], it["im"])]
+            np.testing.assert_allclose(it["R"], ref["R"].astype(np.float64), atol=1e-7)
+            np.testing.assert_allclose(it["t"], ref["t"].astype(np.float64), atol=1e-7)
+            assert it["bbox"] == [float(v) for v in ref["bbox"]]
+            rgb, depth, ml = ds.tree.read(i)
+            assert np.array_equal(rgb, ref["rgb"])
+            assert np.array_equal(depth, (ref["depth_mm"].astype(np.float64) / 1000.0).astype(np.float32))
+            assert np.array_equal(ml, (ref["mask"] == 255).astype(np.uint8))
+            assert ds.crop_size(i) in (80, 120)
+        mp = ds.tree.model_points[6]
+        assert mp.shape == (2600, 3) and np.abs(mp).max() <= 0.05
+    v = ply_vtx(str(tmp_path / "models" / "obj_06.ply"))
+    assert v.shape == (3000, 3) and v.dtype == np.float32
+
+
+def test_linemod_tree_cat_only(tmp_path):
+    from linemod_tree import write_tree
+    from pose_estimation_amd.dataset import BucketBatcher, PoseDataset
+    write_tree(str(tmp_path), objs=(6,), per_obj=4, sizes=(80, 120))
+    ds = PoseDataset("test", 500, False, str(tmp_path), 0.0, 8, cls_type="cat")
+    assert ds.objlist == [6] and len(ds) == 4
+    batches = list(BucketBatcher(ds, 8))
+    assert sorted(S for S, _ in batches) == [80, 120]
+    assert sorted(i for _, idx in batches for i in idx) == [0, 1, 2, 3]

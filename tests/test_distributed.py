@@ -65,3 +65,80 @@ def test_bucket_shard_single_size_per_batch():
     a = kd.bucket_shard(sizes, 4, 0)
     assert a == {120: [0, 1, 2], 160: [10, 11]}
     assert kd.shard_range(10, 4, 3) == (8, 10)
+
+
+class _FakeSet:
+    """Stands in for PoseDataset in the sharded-epoch rehearsal: crop sizes, objects, diameters."""
+    objlist = [1, 2, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15]
+    sym_obj = [7, 8]
+
+    def __init__(self, n):
+        g = torch.Generator().manual_seed(0)
+        self.sizes = [int(s) for s in (torch.randint(1, 6, (n,), generator=g) * 40)]
+        self.diameter = [0.1 + 0.01 * i for i in range(len(self.objlist))]
+
+    def __len__(self):
+        return len(self.sizes)
+
+    def crop_size(self, i):
+        return self.sizes[i]
+
+
+def _fake_records(model, dataset, indices, bs, device, opt_pose=True, with_loss=True):
+    """Deterministic per-crop records (a function of the crop id only), in evaluation order."""
+    from pose_estimation_amd import evaluate as ev
+    rows = []
+    for S, idx in ev._batches(indices, bs):
+        for i in idx:
+            g = torch.Generator().manual_seed(1000 + i)
+            r = torch.rand(len(ev.REC), generator=g, dtype=torch.float64)
+            r[ev._R["crop"]] = i
+            r[ev._R["cls"]] = i % len(dataset.objlist)
+            r[ev._R["add_b"]] *= 0.03
+            r[ev._R["add_f"]] *= 0.03
+            r[ev._R["r_b"]] *= 10
+            r[ev._R["r_f"]] *= 10
+            r[ev._R["t_b"]] *= 0.1
+            r[ev._R["t_f"]] *= 0.1
+            r[ev._R["valid"]] = 1.0
+            rows.append(r)
+    return torch.stack(rows) if rows else torch.zeros((0, len(ev.REC)), dtype=torch.float64)
+
+
+def _epoch_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from pose_estimation_amd import evaluate as ev
+    ev.eval_records = _fake_records
+    kd.init_from_env("gloo")
+    out = ev.test_epoch(None, _FakeSet(n), bs=4, device="cpu")
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_epoch_matches_single():
+    """The sharded test_epoch (bucket_shard -> per-rank records -> all-gather -> fold in global
+    crop order, plus the all_reduce tally check) gives the world-1 result exactly."""
+    from pose_estimation_amd import evaluate as ev
+    n = 37
+    saved = ev.eval_records
+    ev.eval_records = _fake_records
+    try:
+        ref = ev.test_epoch(None, _FakeSet(n), bs=4, device="cpu", world=1, rank=0)
+    finally:
+        ev.eval_records = saved
+    assert ref["test_count"] == n
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_epoch_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, out in res:
+        assert out == ref

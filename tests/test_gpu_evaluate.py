@@ -33,3 +33,41 @@ def test_cal_dis_gt_pose_is_zero(dev):
         add, r, t = cal_dis(metric, data["target_r"], data["target_t"], data, b)
         # angular_distance clamps |q1.q2| to 1 - 1e-7 (metric.py:93-97): identical R reads 0.051 deg
         assert add < 1e-6 and r < 0.06 and t < 1e-6
+
+
+def test_eval_epoch_linemod_tree(dev, tmp_path):
+    """test_epoch over a LineMOD-layout tree on disk (PoseDataset(root=...)): frames decoded and
+    staged per batch, inputs built on the GPU bit-exact vs the numpy oracle of _load_data on the
+    decoded frames, every crop evaluated once."""
+    import numpy as np
+    from linemod_tree import write_tree
+    from oracle import inputs_oracle as io
+    write_tree(str(tmp_path), objs=(6,), per_obj=5, sizes=(80, 120))
+    ds = PoseDataset("test", 500, False, str(tmp_path), 0.0, 8, cls_type="cat")
+    idx = [i for i in range(len(ds)) if ds.crop_size(i) == 80]
+    data = ds.batch(idx, dev)
+    torch.cuda.synchronize()
+    for b, i in enumerate(idx):
+        rgb, depth, ml = ds.tree.read(i)
+        rmin, rmax, cmin, cmax = ds.boxes[i]
+        img, m = io.crop_inputs(rgb, depth, ml, rmin, cmin, rmax - rmin)
+        assert np.array_equal(data["img_croped"][b].cpu().numpy(), img)
+        assert np.array_equal(data["point_mask"][b, 0].cpu().numpy().astype(bool), m)
+    m = KRRN(cfg=make_config(num_cls=1, backbone="w18"))
+    init_weights(m, 0)
+    m = m.to(dev).eval()
+    res = run_epoch(m, ds, bs=4, device=dev)
+    assert res["test_count"] == len(ds) == 5
+    assert res["all_num"][6] == 5
+
+
+def test_eval_epoch_without_opt_pose(dev):
+    """opt_pose=False: test_dis sums the base (PnP) ADD(-S) (trainer.py:245-247)."""
+    ds = PoseDataset("test", 500, False, None, 0.0, 8, cls_type="all", num_frames=6, sizes=[80])
+    m = KRRN(cfg=make_config(num_cls=len(ds.objlist), backbone="w18"))
+    init_weights(m, 0)
+    m = m.to(dev).eval()
+    res = run_epoch(m, ds, bs=4, device=dev, opt_pose=False)
+    tot = sum(res["dis_base_rt"].values())
+    assert res["test_dis"] > 0 and abs(res["test_dis"] - tot / len(ds)) < 1e-12
+    assert sum(res["succ_final_rt"].values()) == 0

@@ -85,3 +85,24 @@ def test_pose_loss_match_oracle(dev):
     assert math.isclose(float(out["loss_add"]), float(ref), rel_tol=1e-5), (float(out["loss_add"]), float(ref))
     tot = sum(float(out[k]) for k in ("loss_xyz", "loss_region", "loss_mask", "loss_normal", "loss_add"))
     assert math.isclose(float(out["loss"]), tot, rel_tol=1e-12)
+
+
+@pytest.mark.gpu
+def test_map_losses_per_crop(dev):
+    """Per-crop terms (the reference's batch-size-1 loop, trainer.py:180-182): crop b of a batch
+    with different valid-pixel counts per crop equals the oracle run on crop b alone."""
+    from pose_estimation_amd.loss import map_losses
+    B = 3
+    pred, gt = _maps(B, 31, 29, 7, 4, seed=5)
+    for k in ("xyz", "normal"):
+        gt[k][1, :, :20] = 0.0  # crop 1: far fewer valid pixels
+    gt["region"][2, :25] = 0
+    gt["multi_cls_mask"][0, :10] = 0
+    got = map_losses({k: v.to(dev) for k, v in pred.items()}, {k: v.to(dev) for k, v in gt.items()}, per_crop=True).cpu()
+    assert got.shape == (B, 8)
+    for b in range(B):
+        ref = lo.krrn_loss({k: v[b:b + 1] for k, v in pred.items()}, {k: v[b:b + 1] for k, v in gt.items()}, SYM_OBJ,
+                           opt_pose=False)
+        for i, k in enumerate(("loss_xyz", "loss_normal", "loss_region", "loss_mask")):
+            assert math.isclose(float(got[b, i]), float(ref[k]), rel_tol=2e-6), (b, k, float(got[b, i]), float(ref[k]))
+        assert int(got[b, 6]) == int((gt["region"][b] != 0).sum())
