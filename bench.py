@@ -152,6 +152,21 @@ def _cpu_model_name() -> str:
     return "unknown"
 
 
+def cpu_quota():
+    """CPUs this process may use: the cgroup v2 quota (cpu.max) when set, else the affinity set.
+    The GPU box reports os.cpu_count() = 256 host CPUs under a 16-CPU quota: 256 torch threads
+    would oversubscribe the quota 16x, so the CPU leg uses the quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def _cpu_config(B: int, S: int, N: int, backbone: str, warmup: int, reps: int, seed: int):
     """crops/s of the CPU oracle (PyTorch-CPU restatement + C EPnP-RANSAC, H = 100, 1 px) on one
     config: `warmup` untimed batches, then the median over `reps` timed batches."""
@@ -197,6 +212,7 @@ def cpu_baseline(S: int, N: int, threads: int, reps2: int, warmup2: int):
     return {"value": c2["value"], "unit": "crops/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model_name(), "os_cpu_count": os.cpu_count(),
             "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "cpu_quota": cpu_quota(),
             "config1": c1, "config2": c2,
             "sample": f"config 2 (value): B=64 'cat' S={S} N={N} HRNet-W18, median of {reps2} batches after {warmup2} "
                       f"warm-up; config 1: B=1 HRNet config.yaml widths, median of 10 after 3; oracle/krrn_oracle.py "
@@ -296,7 +312,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU leg (baseline + accuracy)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="torch threads of the CPU leg (0 = os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="torch threads of the CPU leg (0 = the CPUs this process may use: cgroup quota / affinity)")
     ap.add_argument("--cpu-reps", type=int, default=3, help="timed B=64 CPU batches (BASELINE.md §2 protocol: 10)")
     ap.add_argument("--cpu-warmup", type=int, default=1, help="untimed B=64 CPU batches (protocol: 3)")
     ap.add_argument("--breakdown", default="", help="write the per-kernel breakdown JSON here")
@@ -394,7 +411,7 @@ def main():
     cpu, acc = None, None
     if rank == 0 and world == 1 and step is not None and not args.no_cpu:
         acc = cpu_leg_accuracy(dev)
-        threads = args.cpu_threads or (os.cpu_count() or 1)
+        threads = args.cpu_threads or cpu_quota()
         cpu = cpu_baseline(S, N, threads, args.cpu_reps, args.cpu_warmup)
     if rank == 0:
         line = {

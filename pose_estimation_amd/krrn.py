@@ -313,6 +313,9 @@ class KRRN(nn.Module):
         with torch.no_grad():
             p = KRRNPlan(self, B, S, N, opt_pose, dev)
         self._plans[key] = p
+        # the estimate is a heuristic: enforce the budget with the plan's real size too
+        while len(self._plans) > 1 and self.plans_bytes() > self.plan_budget_bytes:
+            self._plans.popitem(last=False)
         return p
 
     def plans_bytes(self) -> int:

@@ -21,6 +21,10 @@ MAP_RTOL = 2e-4
 # ~2% of the feature rows discretely and pred_t by up to ~6e-6 m; the reference itself would
 # flip the same way between its CPU and GPU runs.
 T_ATOL = 1e-6
+# pred_t between two runs whose pool / idx2 kNN decisions over predicted coordinates differ in a
+# few near-tied rows (measured: 1.2e-5 m for B=64 vs B=2 of the same crops)
+T_ATOL_FLIP = 5e-5
+_DECISIONS = ("pool_v", "pool_x", "pool_n", "pool2", "idx2")
 # per-point feature rows: the fraction whose max error stays under FEAT_RTOL of max|feat|
 FEAT_RTOL, FEAT_ROWS = 1e-3, 1.0
 # argmax near-tie: oracle top-2 logit gap below this fraction of the map's max magnitude
@@ -172,6 +176,7 @@ def test_config2_full_batch(models, dev):
     d = make_batch(B, S, N, seed=31)
     perms = _draw_perms(N, 13)
     out = _check_parity(m, o, dev, B, S, N, d, crops=[0, 31, 63], perms=perms)
+    fb64 = {k: v.cpu() for k, v in m.get_plan(B, S, N, True).fusion_bufs.items() if k in _DECISIONS}
     two = [0, 63]
     d2 = {k: d[k][two] for k in ("img_croped", "cloud", "choose", "cls_id")}
     o2 = m(d2["img_croped"].to(dev), d2["cloud"].to(dev), d2["choose"].to(dev), d2["cls_id"].to(dev),
@@ -181,9 +186,16 @@ def test_config2_full_batch(models, dev):
         e = _rel(out[k][two], o2[k])
         print(f"  B=64 vs B=2 {k}: {e:.2e}")
         assert e < MAP_RTOL, (k, e)
+    # the discrete decisions over *predicted* coordinates (x / n pool kNNs, 9-D idx2) may flip
+    # between the two batch shapes (different tiles / split-K -> different f32 rounding of the
+    # maps); pred_t must agree to T_ATOL when they all agree, to T_ATOL_FLIP otherwise
+    fb2 = m.get_plan(2, S, N, True).fusion_bufs
+    agree = {k: float((fb64[k][two] == fb2[k].cpu()).float().mean()) for k in _DECISIONS}
     e = float((out["pred_t"][two].cpu() - o2["pred_t"].cpu()).abs().max())
-    print(f"  B=64 vs B=2 pred_t: {e:.2e} m")
-    assert e < T_ATOL
+    print(f"  B=64 vs B=2 pred_t: {e:.2e} m, decision agreement {agree}")
+    assert agree["pool_v"] == 1.0 and agree["pool2"] == 1.0
+    assert all(v > 0.99 for v in agree.values()), agree
+    assert e < (T_ATOL if all(v == 1.0 for v in agree.values()) else T_ATOL_FLIP)
     for name in ("mask", "region"):
         n_bad = int((out[name][two].argmax(1) != o2[name].argmax(1)).sum())
         print(f"  B=64 vs B=2 argmax({name}) mismatches: {n_bad}")
