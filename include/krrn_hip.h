@@ -96,6 +96,10 @@ int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* st
 int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* U,
                           int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                           int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
+/* Kernel choice for krrn_conv3x3_wino_f32 (process-wide; default 1, or env KRRN_WINO_V):
+ * 1 = ring-staged raw patches, transform beside the MFMAs; 2 = the same without that overlap;
+ * 0 = the register-staged V image. All three give bit-identical results. */
+int krrn_wino_variant(int v);
 
 /* k nearest neighbours without the [n, n] distance matrix.
  * Replaces gcn3d.get_neighbor_index (gcn3d.py:15-26; mode 0, drop_first = 1: topk(k+1)[1:])

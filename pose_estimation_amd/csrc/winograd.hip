@@ -14,25 +14,30 @@
 // (Lavin & Gray 2016). The 16 products per tile replace 36 multiply-adds of the direct
 // conv: 2.25x fewer MFMA flops. Neither V nor M ever leaves the CU.
 //
-// Block = 32 tiles x 64 output channels, 256 threads = 4 waves; wave w owns components
-// xi = 4w .. 4w+3 over the whole 32 x 64 block (2 x v_mfma_f32_32x32x2_f32 n-blocks each, 128
-// accumulator registers). Input channels stream in chunks of 8: thread (tile, channel) builds
-// the 16 V values from its 4x4 patch (raw buffer loads, out-of-image pixels return 0 = the
-// conv's zero padding; patch offsets precomputed once), weights are staged [xi][n][c]; both
-// k-contiguous in LDS (pitch 12 floats = 3 x 16 B: conflict-free ds_read_b128) so one
-// ds_read_b128 per operand feeds 4 MFMAs. 73.5 KB of LDS -> 2 blocks per CU, so one block's
-// staging overlaps the other's MFMAs; the next chunk's global loads are in flight during the
-// current chunk's MFMAs. The output transform: wave w holds row u = w of every (tile, channel)'s
-// 4x4 M, so the column combination is lane-local and only 2 of 4 values per row go through LDS;
-// stores are float4 channel runs.
-// Measured and rejected (MI355X, 64 x 128 x 120 x 120): double-buffered LDS at one wave per SIMD
-// (2.24 ms vs 1.50), persistent blocks prefetching the next tile during the epilogue (1.57 ms,
-// register spills), s_setprio around the MFMA cluster (+2 %), a 32-wide N tile at 3 blocks/CU
-// (1.54-1.56 ms), s-outer MFMA order / double-buffered fragments (1.51-1.52 ms), the ping-pong
-// kernel below (KRRN_WINO_V=1: 1.95 ms — staging and f32 MFMAs of the two waves on a SIMD do
-// not overlap), LDS-DMA weights (KRRN_WINO_V=2: 1.49 ms, within noise). GRBM_GUI_ACTIVE puts
-// the S=120 launch at 3.15 M cycles per XCD (clock 1.9-2.2 GHz under this load) against 1.84 M
-// cycles of MFMA issue: 58 % of the clock-adjusted f32 matrix peak.
+// Default kernel (wino_f23_ring_kernel): block = 16 x 2 output tiles of one image x 64 output
+// channels, 256 threads = 4 waves; wave w owns the components xi = 4w .. 4w+3 (row u = w of the
+// 4x4 grid) over the whole 32 x 64 block (2 x v_mfma_f32_32x32x2_f32 n-blocks each, 128
+// accumulator registers). Input channels stream in chunks of 8. Per chunk the block stages the
+// RAW input region of its 32 tiles (6 x 34 pixels x 8 channels, one b128 load per 16-B piece, 2
+// per thread, zero outside the image) into a 3-slot LDS ring; each lane reads the 2 patch rows its
+// component row needs (8 ds_read_b128) and forms its MFMA A operands V = B^T d B in registers,
+// for chunk ck+1 while chunk ck's MFMAs issue. A wave's weights are disjoint from the other
+// waves', so they skip LDS: 8 b128 loads per lane per chunk (1 KB contiguous per instruction),
+// one chunk ahead. One barrier per chunk. The output transform: wave w holds row u = w of every
+// (tile, channel)'s 4x4 M, so the column combination is lane-local and only 2 of 4 values per
+// row go through LDS; stores are float4 channel runs. The register-staged kernel
+// (wino_f23_kernel: every thread transforms one (tile, channel) patch into an LDS image of V,
+// weights staged through LDS, two barriers per chunk) stays selectable (krrn_wino_variant(0));
+// both give bit-identical outputs (same V operands, same MFMA order).
+// Measured (MI355X, 64 x 128 -> 128 x 120 x 120, profiles/bench_wino.py): staged 1.55 ms, ring
+// 1.41 ms (84 TF in the matrix pipe; 68 % MFMA-busy by SQ_VALU_MFMA_BUSY_CYCLES at 2.05 GHz,
+// waves 73 % issue-stalled, 10 % in s_waitcnt / barriers), ring without the transform overlap
+// 1.44 ms; the epilogue costs 6-8 % (1.35 ms with it skipped). Rejected: an LDS-free variant
+// (every lane loading its own 8 patch vectors: 1.46 ms, TA busy 2.3x), s-outer MFMA order (no
+// gain), and from round 1: double-buffered LDS at one wave per SIMD (2.24 ms), persistent blocks
+// prefetching the next tile during the epilogue (1.57 ms, spills), s_setprio around the MFMA
+// cluster (+2 %), a 32-wide N tile at 3 blocks/CU (1.54-1.56 ms), a ping-pong kernel with two
+// wave groups (1.95 ms), LDS-DMA weights (1.49 ms).
 #include "krrn_common.h"
 
 #include <cstdlib>
@@ -48,6 +53,9 @@ constexpr int kWT = 32;       // tiles per block
 #endif
 #ifndef KRRN_WINO_EXP
 #define KRRN_WINO_EXP 0
+#endif
+#ifndef KRRN_WINO_SOUTER
+#define KRRN_WINO_SOUTER 0
 #endif
 #ifndef KRRN_WINO_WN
 #define KRRN_WINO_WN 64
@@ -419,132 +427,151 @@ __global__ __launch_bounds__(256, kWBlocks) void wino_f23_kernel(const WinoArgs 
   wino_epilogue(a, smem, acc, t0, n0, HWt);
 }
 
-// Ping-pong variant: 512 threads = two groups of 4 waves, one wave of each group per SIMD, one
-// block per CU with two LDS buffers (144 KB). Group g owns the chunks c = g (mod 2): it stages
-// chunk c into buffer c & 1 during step c-1, while the other group runs the MFMAs of chunk c-1
-// from the other buffer, and runs chunk c's MFMAs during step c. So on every SIMD one wave
-// streams MFMAs while its partner transforms / writes the next chunk (VALU and LDS issue beside
-// the matrix pipe), with ONE barrier per step; each group's loads are in flight for two steps.
-// Both groups hold partial sums over their own chunks for the whole 32 x 64 tile; the epilogue
-// adds them in the (c0, c1) staging layout and all 512 threads finish the output transform.
-constexpr int kPPBuf = 16 * (kWT + kWN) * kWP;  // floats per LDS buffer (A then B)
-static_assert(4 * 2 * kWT * kSP <= 2 * kPPBuf, "epilogue staging must fit");
+// ---- Ring variant (KRRN_WINO_V=3): raw input patches through a 2-slot LDS ring, the
+// transform done by the consuming waves, weights straight to registers --------------------------
+// Block = 16 x 2 output tiles (32 x 4 output pixels of one image) x 64 output channels; wave w
+// owns component row u = w (xi = 4w .. 4w+3) as above. Per 8-channel chunk the block stages the
+// RAW input region its 32 tiles read (6 rows x 34 cols x 8 channels = 408 16-B pieces, 2 per
+// thread, one b128 load each) into a ring slot; each lane then reads the 2 patch rows its
+// component row needs (8 ds_read_b128 = 4 columns x 2 rows x its 4 channels), forms
+// t = B^T-row (d_a +- d_b) and V[v] = t-combinations in registers (the same f32 operations as the
+// staged kernel: bit-identical operands), and feeds them as MFMA A operands. The weights of a
+// wave's own 4 components are disjoint from the other waves', so they skip LDS: 8 b128 loads per
+// lane per chunk (1 KB contiguous per wave-instruction), one chunk ahead. One barrier per chunk.
+constexpr int kGX = 16, kGY = 2;                 // tiles per block (x, y): kGX * kGY == kWT
+constexpr int kRR = 2 * kGY + 2, kRC = 2 * kGX + 2;  // raw rows / cols of a block
+constexpr int kRPieces = kRR * kRC * 2;          // 16-B pieces per chunk
+constexpr int kRSlot = 512 * 4;                  // floats per ring slot (2 pieces per thread)
+static_assert(kGX * kGY == kWT && kRPieces <= 512, "ring geometry");
+static_assert(4 * 2 * kWT * kSP >= 3 * kRSlot, "ring fits in the epilogue's LDS");
 
-__global__ __launch_bounds__(512, 1) void wino_f23_pp_kernel(const WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * kPPBuf];
-  const int grp = threadIdx.x >> 8;
-  int t0, n0, HWt;
-  wino_block(a, t0, n0, HWt);
-  const WinoStager sg(a, t0, n0, HWt, threadIdx.x & 255);
-  f32x16 acc[4][kNJ];
+// epilogue finish for a 2-D tile block: tile tl -> (ty, tx) = (tl / kGX, tl % kGX)
+__device__ __forceinline__ void wino_epi_finish2d(const WinoArgs& a, const float* smem, int b, int ty0, int tx0,
+                                                  int n0) {
+  constexpr int kNP = kWT * kN4 / 256;
+  const int tid = threadIdx.x;
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int i = 0; i < kNP; ++i) {
+    const int pr = tid + 256 * i;
+    const int n4 = pr % kN4, tl = pr / kN4;
+    const int n = n0 + 4 * n4;
+    const int ty = ty0 + tl / kGX, tx = tx0 + tl % kGX;
+    if (ty >= a.Ht || tx >= a.Wt || n >= a.n_store) continue;
+    f32x4 c[4][2];
 #pragma unroll
-    for (int j = 0; j < kNJ; ++j)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
-  float d[16];
-  f32x4 w[kNWF];
-  const int nck = sg.nchunks;
-  sg.load(grp, d, w);
-  if (grp == 0) {  // step -1: group 0 stages chunk 0
-    sg.stage(d, w, smem, smem + 16 * kWT * kWP);
-    sg.load(2, d, w);
-  }
-  __syncthreads();
-  for (int s = 0; s < nck; ++s) {
-    if ((s & 1) == grp) {
-      const float* cur = smem + (s & 1) * kPPBuf;
-      wino_mma(cur, cur + 16 * kWT * kWP, acc);
-    } else if (s + 1 < nck) {
-      float* nxt = smem + ((s + 1) & 1) * kPPBuf;
-      sg.stage(d, w, nxt, nxt + 16 * kWT * kWP);
-      sg.load(s + 3, d, w);  // this group's next chunk (zeros past the last one)
+      for (int q = 0; q < 2; ++q) c[u][q] = *reinterpret_cast<const f32x4*>(smem + ((u * 2 + q) * kWT + tl) * kSP + 4 * n4);
+    f32x4 y[4];
+    y[0] = c[0][0] + c[1][0] + c[2][0];
+    y[1] = c[0][1] + c[1][1] + c[2][1];
+    y[2] = c[1][0] - c[2][0] - c[3][0];
+    y[3] = c[1][1] - c[2][1] - c[3][1];
+    f32x4 scl = {1.f, 1.f, 1.f, 1.f}, bia = {0.f, 0.f, 0.f, 0.f};
+    if (a.vec) {
+      if (a.scale) scl = *reinterpret_cast<const f32x4*>(a.scale + n);
+      if (a.bias) bia = *reinterpret_cast<const f32x4*>(a.bias + n);
     }
-    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+      if (oy >= a.H || ox >= a.W) continue;
+      const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+      if (a.vec) {
+        f32x4 v = y[q] * scl + bia;
+        if (a.res) v += *reinterpret_cast<const f32x4*>(a.res + pix * a.res_cs + a.res_co + n);
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        *reinterpret_cast<f32x4*>(a.out + pix * a.out_cs + a.out_co + n) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (n + e >= a.n_store) break;
+          float v = y[q][e] * (a.scale ? a.scale[n + e] : 1.f) + (a.bias ? a.bias[n + e] : 0.f);
+          if (a.res) v += a.res[pix * a.res_cs + a.res_co + n + e];
+          if (a.relu) v = fmaxf(v, 0.f);
+          a.out[pix * a.out_cs + a.out_co + n + e] = v;
+        }
+      }
+    }
   }
-  if (grp == 1) wino_epi_put<false>(smem, acc);
-  __syncthreads();
-  if (grp == 0) wino_epi_put<true>(smem, acc);
-  __syncthreads();
-  wino_epi_finish<512>(a, smem, t0, n0, HWt);
 }
 
-// LDS-DMA variant: the transformed weights go global -> LDS with global_load_lds (16 B per
-// lane, no VGPR round trip, no ds_write), double-buffered so chunk ck+1's weights stream in
-// during chunk ck's MFMAs; only the input patches are register-staged (their transform needs
-// VALU). LDS images are unpadded with an XOR swizzle of the 16-B half of each 32-B row (bit 3 of
-// the row), which keeps every ds_read_b128 lane group and every ds_write_b32 half-wave
-// conflict-free: A [16][32][8] (16 KB) + B 2 x [16][64][8] (64 KB) = 80 KB -> 2 blocks per CU.
-// The swizzle is applied on the SOURCE address of the DMA (its LDS side is lane-linear).
-constexpr int kGA = 16 * kWT * kWC;  // floats of the A image
-constexpr int kGB = 16 * kWN * kWC;  // floats of one B image
-static_assert(4 * 2 * kWT * kSP <= kGA + 2 * kGB, "epilogue staging must fit");
-static_assert(kWN == 64, "glds B mapping assumes 64 output channels per block");
+template <int PIPE>
+__global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * 2 * kWT * kSP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int gxn = krrn_cdiv(a.Wt, kGX), gyn = krrn_cdiv(a.Ht, kGY), nbn = krrn_cdiv(a.N, kWN);
+  const int per_img = gxn * gyn;
+  const int bid = krrn_xcd_remap(blockIdx.x, a.B * per_img * nbn);
+  const int sp = bid / nbn, nb = bid - (bid / nbn) * nbn;
+  const int b = sp / per_img, r2 = sp - (sp / per_img) * per_img;
+  const int by = r2 / gxn, bx = r2 - (r2 / gxn) * gxn;
+  const int n0 = nb * kWN;
+  const int ty0 = by * kGY, tx0 = bx * kGX;
+  const int nck = krrn_cdiv(a.cin, kWC);
 
-__device__ __forceinline__ int wsw(int row) { return (row >> 3) & 1; }
-
-__device__ __forceinline__ void wino_mma_sw(const float* As, const float* Bs, f32x16 (&acc)[4][kNJ]) {
-  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
-  const int fr = lane & 31, h = lane >> 5;
-  const int ha = 4 * (h ^ wsw(fr));
+  // raw staging: this thread's 2 pieces (pixel q/2 of the block's raw region, channel half q&1)
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.in + (size_t)b * a.img + a.in_co), (short)0, (int)min(a.img * 4 - (long long)a.in_co * 4, 0x7FFFFFFFLL),
+      0x00020000);
+  unsigned roff[2];
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    const int xi = 4 * wave + x;
-    const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWC + ha);
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + 256 * i;
+    const int pix = q >> 1, hh = q & 1;
+    const int rr = pix / kRC, rc = pix - (pix / kRC) * kRC;
+    const int iy = 2 * ty0 - 1 + rr, ix = 2 * tx0 - 1 + rc;
+    const bool ok = q < kRPieces && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    roff[i] = ok ? (unsigned)((((long long)iy * a.W + ix) * a.in_cs + 4 * hh) * 4) : kWOOB;
+  }
+  const int hq0 = tid & 1;  // channel half of piece 0 (piece 1 = tid + 256: the same half)
+  auto load_raw = [&](int ck, f32x4 (&r)[2]) {
+    const unsigned cb = (unsigned)(ck * kWC) * 4u;
+    const unsigned cm = (ck < nck && ck * kWC + 4 * hq0 < a.cin) ? 0u : kWOOB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      r[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (roff[i] + cb) | cm, 0, 0));
+  };
+  auto store_raw = [&](int slot, const f32x4 (&r)[2]) {
+    float* dst = smem + slot * kRSlot;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dst + 4 * (tid + 256 * i)) = r[i];
+  };
+
+  // weights of this wave's components: lane (n = j*32 + fr, channels 4h..4h+3) of U[ck][xi][n]
+  const int fr = lane & 31, h = lane >> 5;
+  const __amdgpu_buffer_rsrc_t rsU = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.U, (short)0, (int)min((long long)nck * 16 * a.N * kWC * 4, 0x7FFFFFFFLL), 0x00020000);
+  unsigned uoff[4][kNJ];
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
 #pragma unroll
     for (int j = 0; j < kNJ; ++j) {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWC + ha);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
+      const int n = n0 + j * 32 + fr;
+      uoff[v][j] = n < a.N ? (unsigned)((((long long)(4 * wave + v) * a.N + n) * kWC + 4 * h) * 4) : kWOOB;
     }
-  }
-}
+  const unsigned ustride = (unsigned)(16 * a.N * kWC * 4);
+  auto load_w = [&](int ck, f32x4 (&w)[4][kNJ]) {
+    const unsigned wb = (unsigned)ck * ustride;
+    const unsigned wm = ck < nck ? 0u : kWOOB;
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j)
+        w[v][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, (uoff[v][j] + wb) | wm, 0, 0));
+  };
 
-__global__ __launch_bounds__(256, 2) void wino_f23_glds_kernel(const WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[kGA + 2 * kGB];
-  float* As = smem;
-  float* Bs0 = smem + kGA;
-  int t0, n0, HWt;
-  wino_block(a, t0, n0, HWt);
-  const WinoStager sg(a, t0, n0, HWt, threadIdx.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // this thread's DMA slots: instruction i covers 16-B slots (4i + wave) * 64 + lane of the B
-  // image = (xi = 2i + wave/2, n = 32 (wave & 1) + lane/2, stored half lane & 1)
-  const int bn = 32 * (wave & 1) + (lane >> 1);
-  const int bh = (lane & 1) ^ wsw(bn);
-  const int gn = min(n0 + bn, a.N - 1);  // rows past N feed output channels that are never stored
-  const float* gB = a.U + ((long long)(wave >> 1) * a.N + gn) * kWC + 4 * bh;
-  const long long gstride_i = 2LL * a.N * kWC;       // floats between instruction i and i+1
-  const long long gstride_ck = 16LL * a.N * kWC;     // floats per chunk
-  auto dma_B = [&](int ck, float* Bs) {
-    const float* g = gB + ck * gstride_ck;
-#pragma unroll
-    for (int i = 0; i < kNWF; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(g + i * gstride_i),
-                                       (__attribute__((address_space(3))) void*)(Bs + ((4 * i + wave) * 64) * 4), 16,
-                                       0, 0);
-  };
-  // A write position of this thread's (tile st, channel sc) value, component xi: row xi*32+st
-  const int aw = sg.st * kWC + (sg.sc ^ (4 * wsw(sg.st)));
-  auto stageA = [&](const float (&d)[16]) {
-    float t[16];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
-      t[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
-      t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
-      t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      As[(u * 4 + 0) * kWT * kWC + aw] = t[u * 4 + 0] - t[u * 4 + 2];
-      As[(u * 4 + 1) * kWT * kWC + aw] = t[u * 4 + 1] + t[u * 4 + 2];
-      As[(u * 4 + 2) * kWT * kWC + aw] = t[u * 4 + 2] - t[u * 4 + 1];
-      As[(u * 4 + 3) * kWT * kWC + aw] = t[u * 4 + 1] - t[u * 4 + 3];
-    }
-  };
+  // this lane's patch rows: t_u = d[ra] + sgn * d[rb] (B^T row u)
+  const int ra = wave == 0 ? 0 : (wave == 2 ? 2 : 1);
+  const int rb = wave == 0 ? 2 : (wave == 3 ? 3 : (wave == 1 ? 2 : 1));
+  const float sgn = wave == 1 ? 1.f : -1.f;
+  const int tx = fr % kGX, ty = fr / kGX;
+  const int pa = ((2 * ty + ra) * kRC + 2 * tx) * 2 + h;  // piece index of (row ra, col 0)
+  const int pb = ((2 * ty + rb) * kRC + 2 * tx) * 2 + h;
+
   f32x16 acc[4][kNJ];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
@@ -552,24 +579,119 @@ __global__ __launch_bounds__(256, 2) void wino_f23_glds_kernel(const WinoArgs a)
     for (int j = 0; j < kNJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
-  float d[16];
-  dma_B(0, Bs0);
-  sg.loadA(0, d);
-  const int nck = sg.nchunks;
-  for (int ck = 0; ck < nck; ++ck) {
-    stageA(d);
-    __syncthreads();  // A(ck) written, B(ck) landed (the barrier drains the DMA)
-    if (ck + 1 < nck) {
-      dma_B(ck + 1, Bs0 + ((ck + 1) & 1) * kGB);
-      sg.loadA(ck + 1, d);
+
+  auto make_v = [&](const float* sl, f32x4 (&V)[4]) {
+    f32x4 t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 da = *reinterpret_cast<const f32x4*>(sl + 4 * (pa + 2 * c));
+      const f32x4 db = *reinterpret_cast<const f32x4*>(sl + 4 * (pb + 2 * c));
+      t[c] = da + sgn * db;
     }
-    wino_mma_sw(As, Bs0 + (ck & 1) * kGB, acc);
+    V[0] = t[0] - t[2];
+    V[1] = t[1] + t[2];
+    V[2] = t[2] - t[1];
+    V[3] = t[1] - t[3];
+  };
+  auto mma = [&](const f32x4 (&V)[4], const f32x4 (&wc)[4][kNJ]) {
+#if KRRN_WINO_SOUTER
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int j = 0; j < kNJ; ++j)
+          acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(V[v][s2], wc[v][j][s2], acc[v][j], 0, 0, 0);
+#else
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+          acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(V[v][s2], wc[v][j][s2], acc[v][j], 0, 0, 0);
+#endif
+  };
+
+  f32x4 raw[2];
+  f32x4 w[4][kNJ];
+  if constexpr (PIPE == 0) {
+    load_raw(0, raw);
+    load_w(0, w);
+    store_raw(0, raw);
+    load_raw(1, raw);
     __syncthreads();
+    for (int ck = 0; ck < nck; ++ck) {
+      f32x4 V[4];
+      make_v(smem + (ck & 1) * kRSlot, V);
+      f32x4 wc[4][kNJ];
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int j = 0; j < kNJ; ++j) wc[v][j] = w[v][j];
+      load_w(ck + 1, w);
+      mma(V, wc);
+      store_raw((ck + 1) & 1, raw);
+      load_raw(ck + 2, raw);
+      __syncthreads();
+    }
+  } else {
+    // 3-slot ring: V of chunk ck+1 is formed (LDS reads + transform) beside chunk ck's MFMAs
+    load_raw(0, raw);
+    load_w(0, w);
+    store_raw(0, raw);
+    load_raw(1, raw);
+    __syncthreads();
+    store_raw(1, raw);
+    load_raw(2, raw);
+    f32x4 V[4];
+    make_v(smem, V);
+    __syncthreads();
+    for (int ck = 0; ck < nck; ++ck) {
+      f32x4 wc[4][kNJ];
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int j = 0; j < kNJ; ++j) wc[v][j] = w[v][j];
+      load_w(ck + 1, w);
+      f32x4 Vn[4];
+      make_v(smem + ((ck + 1) % 3) * kRSlot, Vn);
+      mma(V, wc);
+      store_raw((ck + 2) % 3, raw);
+      load_raw(ck + 3, raw);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) V[v] = Vn[v];
+      __syncthreads();
+    }
   }
-  wino_epilogue(a, smem, acc, t0, n0, HWt);
+#if KRRN_WINO_EXP == 4  // timing experiment: one store per lane instead of the epilogue
+  float sum = 0.f;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) sum += acc[x][j][0] + acc[x][j][15];
+  if (sum == 12345.f) a.out[tid] = sum;
+  return;
+#endif
+  wino_epi_put(smem, acc);
+  __syncthreads();
+  wino_epi_finish2d(a, smem, b, ty0, tx0, n0);
 }
 
 }  // namespace
+
+// kernel choice (krrn_wino_variant): 1 = the ring kernel with the next chunk's transform beside
+// the MFMAs (default), 2 = the ring kernel without that overlap, 0 = the register-staged kernel
+static int g_wino_variant = [] {
+  const char* e = getenv("KRRN_WINO_V");
+  return e ? atoi(e) : 1;
+}();
+
+KRRN_API int krrn_wino_variant(int v) {
+  if (v < 0 || v > 2) return KRRN_EARG;
+  g_wino_variant = v;
+  return KRRN_OK;
+}
 
 KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
                                    const float* U, int N, int n_store, const float* scale, const float* bias,
@@ -599,15 +721,15 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   if (span >= 0x7FFF0000LL || (long long)krrn_cdiv(cin, kWC) * 16 * N * kWC * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long blocks = (long long)krrn_cdiv(a.T, kWT) * krrn_cdiv(N, kWN);
   if (blocks > 0x7fffffffLL) return KRRN_ESHAPE;
-  static const int variant = [] {  // 0: register-staged, 1: ping-pong, 2: LDS-DMA weights
-    const char* e = getenv("KRRN_WINO_V");
-    return e ? atoi(e) : 0;
-  }();
-  if (variant == 1)
-    hipLaunchKernelGGL(wino_f23_pp_kernel, dim3((unsigned)blocks), dim3(512), 0, (hipStream_t)stream, a);
-  else if (variant == 2 && N % kWN == 0)
-    hipLaunchKernelGGL(wino_f23_glds_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-  else
+  if (g_wino_variant == 0) {
     hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  } else {
+    const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kWN);
+    if (rb > 0x7fffffffLL || a.img * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
+    if (g_wino_variant == 2)
+      hipLaunchKernelGGL(wino_f23_ring_kernel<0>, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(wino_f23_ring_kernel<1>, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
+  }
   return krrn_launch_status();
 }

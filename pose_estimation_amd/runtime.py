@@ -43,6 +43,7 @@ _lib.register("krrn_ransac_subsets", [P, U, I, I, I, P, P])
 _lib.register("krrn_rng_advance", [P, P])
 _lib.register("krrn_conv2d_group_f32", [P, I, I, P])
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
+_lib.register("krrn_wino_variant", [I])
 
 
 class ConvDesc(ctypes.Structure):

@@ -181,7 +181,7 @@ def test_conv_group_matches_single(dev, tile):
 
 
 @pytest.mark.parametrize("cin,cout,H,W,co", [(128, 128, 30, 30, 0), (64, 72, 17, 23, 4), (272, 272, 15, 15, 0),
-                                             (36, 40, 9, 8, 8)])
+                                             (36, 40, 9, 8, 8), (20, 132, 61, 35, 0), (128, 64, 120, 120, 0)])
 def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     """Fused Winograd F(2x2,3x3) (odd sizes, channel-offset input, residual) vs torch fp32 conv."""
     from pose_estimation_amd import _lib
@@ -203,10 +203,22 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     ra = _nhwc(res, dev)
     out = ops.new_act(B, H, W, cout, dev, cs=ops.pad4(cout) + 4)
     np_ = ops.pad4(cout)
-    _lib.check(_lib.lib().krrn_conv3x3_wino_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U), np_, np_,
-                                                ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
-                                                out.cs, 0, 1, P(torch.cuda.current_stream().cuda_stream)), "wino")
-    torch.cuda.synchronize()
-    got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    L = _lib.lib()
+    outs = []
+    try:
+        for variant in (1, 0, 2):  # ring + overlapped transform (default), register-staged, ring
+            _lib.check(L.krrn_wino_variant(variant), "krrn_wino_variant")
+            out.t.fill_(float("nan") if variant else 0.0)
+            out.t[..., np_:] = 0.0
+            _lib.check(L.krrn_conv3x3_wino_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U), np_, np_,
+                                               ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
+                                               out.cs, 0, 1, P(torch.cuda.current_stream().cuda_stream)), "wino")
+            torch.cuda.synchronize()
+            outs.append(out.t.clone())
+    finally:
+        L.krrn_wino_variant(1)
+    got = outs[0][..., :cout].permute(0, 3, 1, 2).cpu()
     torch.testing.assert_close(got, ref, **TOL)
-    assert torch.count_nonzero(out.t[..., np_:]).item() == 0
+    assert torch.count_nonzero(outs[0][..., np_:]).item() == 0
+    # the three kernels are bit-identical (same V operands and MFMA order), every output written
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
