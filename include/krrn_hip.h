@@ -32,6 +32,7 @@ extern "C" {
 #define KRRN_EARG (-1)
 #define KRRN_ESHAPE (-2)
 #define KRRN_EALIGN (-3)
+#define KRRN_EUNSUPPORTED (-4) /* the vendor library (hipBLASLt) rejected the problem */
 
 /* Implicit-GEMM convolution / GEMM on the f32 matrix cores, BN folded into scale/bias.
  * Replaces nn.Conv2d + BatchNorm2d (+ residual add) (+ ReLU) of BasicBlock / Bottleneck /
@@ -85,6 +86,21 @@ typedef struct krrn_conv_desc {
  * resolution, so the branches are independent until the fuse layer). Each problem computes
  * exactly what krrn_conv2d_f32 would with the same descriptor. */
 int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* stream);
+
+/* Plain f32 GEMM on hipBLASLt (library-shaped GEMMs of the fusion / TBase, see blas.hip):
+ *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n*K + k] + bias[n] + res[m*ldr + n]),  0 <= n < N
+ * in `batch` strided groups of M rows (A / out / res advance a_grp / o_grp / r_grp floats per
+ * group, W [N][K] shared). create: heuristic query once, the plan is caller-owned (destroy frees
+ * it); *ws_bytes = the workspace run() needs (<= max_ws). run: one hipblasLtMatmul on `stream`
+ * (graph-capturable); bias / res must be given iff the plan was created with them.
+ * KRRN_EUNSUPPORTED when hipBLASLt has no algorithm or fails. */
+typedef struct krrn_blas_gemm krrn_blas_gemm;
+int krrn_blas_gemm_create(int M, int N, int K, int lda, int ldo, int batch, long long a_grp, long long o_grp,
+                          int has_bias, int relu, int has_res, int ldr, long long r_grp, long long max_ws,
+                          krrn_blas_gemm** out_plan, long long* ws_bytes);
+int krrn_blas_gemm_run(const krrn_blas_gemm* g, const float* a, const float* w, const float* bias, const float* res,
+                       float* out, void* workspace, long long ws_bytes, void* stream);
+int krrn_blas_gemm_destroy(krrn_blas_gemm* g);
 
 /* 3x3 stride-1 pad-1 convolution by fused Winograd F(2x2, 3x3) (the head / last_layer /
  * deconv-BasicBlock convs: krrn.py:46-84, myhrnet.py:324-346; cuDNN / MIOpen use the same

@@ -21,7 +21,8 @@ _lib = None
 
 _ERRORS = {-1: "KRRN_EARG (null pointer / bad argument)",
            -2: "KRRN_ESHAPE (dimension outside the supported range)",
-           -3: "KRRN_EALIGN (16-byte alignment / channel stride violation)"}
+           -3: "KRRN_EALIGN (16-byte alignment / channel stride violation)",
+           -4: "KRRN_EUNSUPPORTED (hipBLASLt rejected the problem)"}
 
 # name -> (argtypes). Every entry point returns int.
 _P = ctypes.c_void_p

@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .runtime import Late, Plan, add_conv, ptr
+from .runtime import Late, Plan, add_conv, add_gemm, ptr
 
 
 class Conv_surface(nn.Module):  # noqa: N801 (reference class name, gcn3d.py:72)
@@ -168,6 +168,10 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
                                cin_p=ops.pad4(layer.in_channel))
         keep.append(spec)
         np_ = ops.pad4(spec.cout)
+        if add_gemm(plan, a=a, a_off=a_co, lda=a_cs, M=M, wt=spec.wt[0], K=spec.cin_p, N=np_, scale=spec.scale,
+                    bias=spec.bias, out=out, ldo=out.shape[-1], relu=False, cin=spec.cin, cout=spec.cout,
+                    tag="gcn_gemm"):
+            return
         add_conv(plan, x=ptr(a), x_cs=a_cs, x_co=a_co, B=1, Hi=1, Wi=M, cin_p=spec.cin_p, Hg=1, Wg=M, in_s=1,
                  taps=[(0, 0)], wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
                  out=ptr(out), out_cs=out.shape[-1], out_co=0, Ho=1, Wo=M, cin=spec.cin, cout=spec.cout,

@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .runtime import Late, Plan, add_conv, ptr
+from .runtime import Late, Plan, add_conv, add_gemm, ptr
 
 
 class TBase(nn.Module):
@@ -54,6 +54,13 @@ def emit_tbase_level1(tb: TBase, plan: Plan, B: int, N: int, N1: int, feat1: tor
     wc = ops.make_linear(w1[:, 896:1280], None, None, dev)
     Q = plan.buf((B * N1, np1))
     P1 = plan.buf((B * N1, np1))
+    if add_gemm(plan, a=feat2, a_off=0, lda=384, M=B * N1, wt=wc.wt[0], K=wc.cin_p, N=np1, scale=wc.scale,
+                bias=wc.bias, out=Q, ldo=np1, relu=False, cin=wc.cin, cout=wc.cout, tag="tbase_gemm") and \
+            add_gemm(plan, a=feat1, a_off=0, lda=384, M=N1, wt=wb.wt[0], K=wb.cin_p, N=np1, scale=wb.scale,
+                     bias=wb.bias, out=P1, ldo=np1, relu=False, res=Q, ldr=np1, batch=B, a_grp=N * 384,
+                     o_grp=N1 * np1, r_grp=N1 * np1, cin=wb.cin, cout=wb.cout, tag="tbase_gemm"):
+        plan.buffers.append([wb, wc])
+        return dict(P1=P1, Q=Q)
     add_conv(plan, x=ptr(feat2), x_cs=384, x_co=0, B=1, Hi=1, Wi=B * N1, cin_p=wc.cin_p, Hg=1, Wg=B * N1, in_s=1,
              taps=[(0, 0)], wt=ptr(wc.wt[0]), N=np1, n_store=np1, scale=ptr(wc.scale), bias=ptr(wc.bias),
              out=ptr(Q), out_cs=np1, out_co=0, Ho=1, Wo=B * N1, relu=False, cin=wc.cin, cout=wc.cout,
@@ -101,6 +108,10 @@ def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, 
 
     def gemm(a, K, spec, out, bias2=None, rows=M, relu=True):
         np_ = ops.pad4(spec.cout)
+        if bias2 is None and add_gemm(plan, a=a, a_off=0, lda=K, M=rows, wt=spec.wt[0], K=spec.cin_p, N=np_,
+                                      scale=spec.scale, bias=spec.bias, out=out, ldo=out.shape[-1], relu=relu,
+                                      cin=spec.cin, cout=spec.cout, tag="tbase_gemm"):
+            return
         add_conv(plan, x=ptr(a), x_cs=K, x_co=0, B=1, Hi=1, Wi=rows, cin_p=spec.cin_p, Hg=1, Wg=rows, in_s=1,
                  taps=[(0, 0)], wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
                  bias2=ptr(bias2) if bias2 is not None else None, b2_div=N, out=ptr(out), out_cs=out.shape[-1],

@@ -44,6 +44,9 @@ _lib.register("krrn_rng_advance", [P, P])
 _lib.register("krrn_conv2d_group_f32", [P, I, I, P])
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_wino_variant", [I])
+_lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L, P, P])
+_lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
+_lib.register("krrn_blas_gemm_destroy", [P])
 
 
 class ConvDesc(ctypes.Structure):
@@ -327,3 +330,52 @@ def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str 
     plan.add("krrn_conv2d_group_f32", ctypes.cast(arr, P), n, tile,
              meta=dict(kernel=f"conv_group<{','.join(map(str, TILE_SHAPES[tile]))}>", flops=flops, tag=tag,
                        M=shapes[0][0], N=shapes[0][1], K=shapes[0][2], splits=nsplit, shapes=shapes))
+
+
+BLAS = os.environ.get("KRRN_BLAS", "1") == "1"
+BLAS_MAX_WS = 64 << 20
+
+
+class _BlasPlan:
+    """Owns one krrn_blas_gemm plan (destroyed with the launch plan that keeps it)."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def __del__(self):
+        try:
+            if self.handle:
+                _lib.lib().krrn_blas_gemm_destroy(self.handle)
+        except Exception:  # interpreter shutdown
+            pass
+
+
+def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: torch.Tensor, K: int, N: int,
+             scale: Optional[torch.Tensor], bias: Optional[torch.Tensor], out: torch.Tensor, ldo: int, relu: bool,
+             res: Optional[torch.Tensor] = None, ldr: int = 0, batch: int = 1, a_grp: int = 0, o_grp: int = 0,
+             r_grp: int = 0, cin: Optional[int] = None, cout: Optional[int] = None, tag: str = "gemm") -> bool:
+    """Append a plain GEMM out[m, n] = act(scale[n] * (A[m] . wt[n]) + bias[n] (+ res[m, n])) on hipBLASLt
+    (krrn_blas_gemm_*; scale folded into the weights). Returns False when hipBLASLt is disabled
+    (KRRN_BLAS=0) or rejects the problem: the caller then emits its own kernel."""
+    if not BLAS:
+        return False
+    dev = plan.device
+    w = wt.reshape(N, -1)[:, :K].float()
+    if scale is not None:
+        w = w * scale.reshape(N, 1).to(w.device)
+    w = w.contiguous()
+    h = ctypes.c_void_p()
+    wsb = ctypes.c_longlong()
+    st = _lib.lib().krrn_blas_gemm_create(M, N, K, lda, ldo, batch, a_grp, o_grp, int(bias is not None), int(relu),
+                                          int(res is not None), ldr, r_grp, BLAS_MAX_WS, ctypes.byref(h),
+                                          ctypes.byref(wsb))
+    if st != 0:
+        return False
+    owner = _BlasPlan(h)
+    ws = plan.buf((max(int(wsb.value), 16),), torch.uint8, zero=False)
+    plan.buffers.append([owner, w, bias])
+    a_ptr = P(a.data_ptr() + 4 * a_off)
+    plan.add("krrn_blas_gemm_run", h, a_ptr, ptr(w), ptr(bias), ptr(res), ptr(out), ptr(ws), int(wsb.value),
+             meta=dict(kernel="hipblaslt_gemm_f32", flops=2.0 * (cin or K) * (cout or N) * M * batch, tag=tag,
+                       M=M * batch, N=N, K=K, splits=1))
+    return True
