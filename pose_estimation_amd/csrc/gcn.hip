@@ -13,13 +13,13 @@
 //   krrn_pool_max_f32   Pool_layer's max over the 4 neighbours (gcn3d.py:233-236), evaluated
 //                       only at the randperm-sampled rows that the reference keeps (:238-241).
 #include <math.h>
+#include <stdlib.h>
 
 #include "krrn_common.h"
 
 namespace {
 
 constexpr int kKnnThreads = 256;
-constexpr int kKnnParts = 4;     // lanes per query, each scanning every 4th candidate
 constexpr int kKnnChunk = 1024;  // candidates per LDS stage
 constexpr int kKnnKmax = 16;
 
@@ -51,24 +51,26 @@ __device__ __forceinline__ bool knn_less(float d0, int i0, float d1, int i1) {
   return d0 < d1 || (d0 == d1 && i0 < i1);
 }
 
-// One query = kKnnParts adjacent lanes. Lane `part` keeps the ascending top-KS of candidates
-// j = part (mod kKnnParts) in registers (KS = k + drop rounded up to an instantiated size);
+// One query = PARTS adjacent lanes. Lane `part` keeps the ascending top-KS of candidates
+// j = part (mod PARTS) in registers (KS = k + drop rounded up to an instantiated size);
 // the partial lists are then merged in (d, index) order, which equals the global stable
-// top-KS because (d, index) is a total order. Block = 64 queries.
-template <int D, int KS>
+// top-KS because (d, index) is a total order. Block = 256 / PARTS queries. PARTS = 4 for the
+// N x N level-0 search; 16 where a crop has few queries (the pools' N/4 sampled rows, level 1/2),
+// so the grid still covers the CUs and each lane's serial scan is 4x shorter.
+template <int D, int KS, int PARTS>
 __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
     const float* __restrict__ q, long long q_bs, int q_st, int nq, const int* __restrict__ qidx,
     const float* __restrict__ c, long long c_bs, int c_st, int nc, int K, int drop, int mode,
     int* __restrict__ out) {
 #pragma clang fp contract(off)
   constexpr int DP = D == 3 ? 4 : 12;  // LDS record: coords + |c|^2 (+ pad)
-  constexpr int QPB = kKnnThreads / kKnnParts;
+  constexpr int QPB = kKnnThreads / PARTS;
   constexpr int STAGE = kKnnChunk * DP;
   constexpr int MERGE = kKnnThreads * KS * 2;
   __shared__ __attribute__((aligned(16))) float sc[STAGE > MERGE ? STAGE : MERGE];
   const int b = blockIdx.y;
-  const int part = threadIdx.x % kKnnParts;
-  const int ql = threadIdx.x / kKnnParts;
+  const int part = threadIdx.x % PARTS;
+  const int ql = threadIdx.x / PARTS;
   const int t = blockIdx.x * QPB + ql;
   const bool active = t < nq;
   float qp[D];
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
       dst[D] = knn_sqnorm<D>(p);
     }
     __syncthreads();
-    for (int j = part; j < cnt; j += kKnnParts) {
+    for (int j = part; j < cnt; j += PARTS) {
       const float* p = sc + j * DP;
       const float inner = knn_inner<D>(qp, p);
       const float cn = p[D];
@@ -137,17 +139,17 @@ __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
   }
   __syncthreads();
   if (!active || part != 0) return;
-  const int base = threadIdx.x * KS;  // lists of lanes threadIdx.x .. threadIdx.x + 3
-  int hp[kKnnParts];
+  const int base = threadIdx.x * KS;  // lists of lanes threadIdx.x .. threadIdx.x + PARTS - 1
+  int hp[PARTS];
 #pragma unroll
-  for (int r = 0; r < kKnnParts; ++r) hp[r] = 0;
+  for (int r = 0; r < PARTS; ++r) hp[r] = 0;
   const int ko = K - drop;
   int* o = out + ((long long)b * nq + t) * ko;
   for (int s2 = 0; s2 < K; ++s2) {
     float best_d = INFINITY;
     int best_i = 0x7fffffff, best_r = 0;
 #pragma unroll
-    for (int r = 0; r < kKnnParts; ++r) {
+    for (int r = 0; r < PARTS; ++r) {
       if (hp[r] < KS) {
         const float dd = md[base + r * KS + hp[r]];
         const int ii = mi[base + r * KS + hp[r]];
@@ -155,16 +157,17 @@ __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
       }
     }
 #pragma unroll
-    for (int r = 0; r < kKnnParts; ++r) hp[r] += (r == best_r);
+    for (int r = 0; r < PARTS; ++r) hp[r] += (r == best_r);
     if (s2 >= drop) o[s2 - drop] = best_i;
   }
 }
 
-template <int D>
-void knn_launch(dim3 grid, hipStream_t s, const float* q, long long q_bs, int q_st, int nq, const int* qidx,
+template <int D, int PARTS>
+void knn_launch(int B, hipStream_t s, const float* q, long long q_bs, int q_st, int nq, const int* qidx,
                 const float* c, long long c_bs, int c_st, int nc, int K, int drop, int mode, int* out) {
-#define KNN_CASE(KS)                                                                                   \
-  hipLaunchKernelGGL((knn_kernel<D, KS>), grid, dim3(kKnnThreads), 0, s, q, q_bs, q_st, nq, qidx, c, c_bs, \
+  const dim3 grid(krrn_cdiv(nq, kKnnThreads / PARTS), B);
+#define KNN_CASE(KS)                                                                                          \
+  hipLaunchKernelGGL((knn_kernel<D, KS, PARTS>), grid, dim3(kKnnThreads), 0, s, q, q_bs, q_st, nq, qidx, c, c_bs, \
                      c_st, nc, K, drop, mode, out)
   if (K <= 1) KNN_CASE(1);
   else if (K <= 2) KNN_CASE(2);
@@ -186,12 +189,26 @@ KRRN_API int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, cons
   if (k + (drop_first ? 1 : 0) > nc) return KRRN_ESHAPE;
   if (mode != 0 && mode != 1) return KRRN_EARG;
   const int K = k + (drop_first ? 1 : 0);
-  dim3 grid(krrn_cdiv(nq, kKnnThreads / kKnnParts), B);
   hipStream_t s = (hipStream_t)stream;
-  if (d == 3)
-    knn_launch<3>(grid, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, drop_first ? 1 : 0, mode, out);
-  else
-    knn_launch<9>(grid, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, drop_first ? 1 : 0, mode, out);
+  const int dr = drop_first ? 1 : 0;
+  // lanes per query: 16 when 4 lanes would leave the grid under ~4 blocks per CU (few queries
+  // per crop) AND every lane still scans >= 48 candidates (the 16-list merge is serial): the
+  // pools' N/4 sampled rows against N candidates (57 -> 34 us at B = 64, N = 1000); the level-0
+  // N x N search and the short level-1 / 2 / nearest scans keep 4 (profiles/bench_knn.py;
+  // KRRN_KNN_PARTS overrides)
+  static const int force = [] {
+    const char* e = getenv("KRRN_KNN_PARTS");
+    return e ? atoi(e) : 0;
+  }();
+  const long long blocks4 = (long long)krrn_cdiv(nq, kKnnThreads / 4) * B;
+  const bool wide = force ? force == 16 : (blocks4 < 1024 && nc >= 16 * 48);
+  if (d == 3) {
+    if (wide) knn_launch<3, 16>(B, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, dr, mode, out);
+    else knn_launch<3, 4>(B, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, dr, mode, out);
+  } else {
+    if (wide) knn_launch<9, 16>(B, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, dr, mode, out);
+    else knn_launch<9, 4>(B, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, dr, mode, out);
+  }
   return krrn_launch_status();
 }
 

@@ -1,0 +1,36 @@
+"""Micro-bench: krrn_knn_f32 on the fusion's shapes (B = 64, N = 1000), 4 vs 16 lanes per query
+(KRRN_KNN_PARTS is read once per process: run with PARTS=4 and PARTS=16 in turn); prints a checksum
+of the indices so both runs can be compared for equality."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pose_estimation_amd import _lib  # noqa: E402
+from pose_estimation_amd.runtime import P, ptr  # noqa: E402
+
+dev = torch.device("cuda", 0)
+B, N = 64, 1000
+g = torch.Generator().manual_seed(0)
+pts = torch.rand(B, N, 9, generator=g).to(dev)
+perm = torch.randperm(N, generator=g)[:250].int().to(dev)
+st = P(torch.cuda.current_stream().cuda_stream)
+# (name, nq, qidx, nc, d, k, drop, mode)
+cases = [("level0 idx0", 1000, None, 1000, 3, 10, 1, 0), ("pool k4", 250, perm, 1000, 3, 4, 1, 0),
+         ("level1 idx1", 250, None, 250, 3, 10, 1, 0), ("level2 idx2 9-D", 62, None, 62, 9, 7, 1, 0),
+         ("nn1", 1000, None, 250, 3, 1, 0, 1), ("nn2", 1000, None, 62, 3, 1, 0, 1)]
+for name, nq, qidx, nc, d, k, drop, mode in cases:
+    out = torch.zeros(B, nq, k, dtype=torch.int32, device=dev)
+    fn = lambda: _lib.check(_lib.lib().krrn_knn_f32(ptr(pts), N * 9, 9, nq, ptr(qidx), ptr(pts), N * 9, 9, nc, d, k,  # noqa: E731
+                                                    drop, mode, B, ptr(out), st), "knn")
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(20):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    cs = int((out.long() * torch.arange(out.numel(), device=dev).view_as(out).remainder(9973)).sum())
+    print(f"{name:18s} {a.elapsed_time(b) / 20 * 1e3:8.1f} us  checksum {cs}", flush=True)
