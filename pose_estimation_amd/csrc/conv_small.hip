@@ -1,0 +1,284 @@
+// Direct 3x3 / stride 1 / pad 1 convolution for the narrow HRNet branch convs (BasicBlock
+// conv1 / conv2 of the 18/36/72/144-channel branches at S/4 .. S/32, lib/network/hrnet/
+// myhrnet.py:34-63), fused with eval-BN scale / bias, the residual add and ReLU.
+//
+// These convs are tiny (0.3-0.7 GFLOP at B = 64) and were bound by per-k-tile load latency in the
+// implicit-GEMM kernel (a wave's 6-40 k-tiles each wait for an im2col gather; 21 us per launch
+// for ~3 us of matrix work). Here a block stages the input rows its 64 output pixels read — all
+// input channels, with a zero border — into LDS ONCE, and then runs the whole K = 9 x cin
+// reduction out of LDS: one global-load phase per block instead of one per k-tile.
+//
+// Block = 256 threads = 4 waves = 64 consecutive output pixels in (b, y, x) raster order (any
+// number of images / rows; e.g. 4 whole 4x4 images, or 2.1 rows of a 30-wide image) x NW
+// 16-channel output tiles. Wave w owns pixels [16w, 16w + 16) of the block and accumulates NW
+// v_mfma_f32_16x16x4_f32 tiles (16 pixels x 16 channels each): 16x16 tiles give 4x the waves of
+// 32x32 tiles for the same output, which is what these small-M / small-N problems need to cover
+// the CUs. Per (tap, 16-channel group): lane (pixel m = l % 16, quad g = l / 16) reads the 4
+// channels 4g..4g+3 of its input pixel from LDS (one ds_read_b128 feeds 4 MFMAs: MFMA s sums
+// k = 4g + s over the 4 lane groups) and the matching weight quad of output channel n = l % 16
+// straight from global memory (the weights are read by every block: L2-resident).
+//
+// Numerics: f32 operands, f32 accumulation (v_mfma_f32_16x16x4_f32 is an fma chain); the k order
+// differs from the implicit-GEMM kernel's, so results agree with it to f32 rounding.
+#include "krrn_common.h"
+
+namespace {
+
+struct SmallArgs {
+  const float* in;
+  int in_cs, in_co;
+  int B, H, W, cin;      // cin = physical channels (multiple of 4)
+  const float* wt;       // [N][9 * cin], k = tap * cin + c, tap = ky * 3 + kx
+  int N, n_store;
+  const float* scale;
+  const float* bias;
+  const float* res;
+  int res_cs, res_co;
+  float* out;
+  int out_cs, out_co;
+  int relu;
+  int M;                 // B * H * W
+  int q;                 // channel quads per pixel (cin / 4)
+  int pitch;             // LDS float4 per staged pixel: q rounded up to odd (conflict-free reads)
+};
+
+constexpr unsigned kOOB = 0xFFFFFFF0u;
+
+// Block = 256 threads = 4 waves over PM = 4 / KS m-tiles (16 output pixels each, consecutive in
+// (b, y, x) raster order) x NW 16-channel n-tiles; wave w computes m-tile w / KS over the K-slice
+// w % KS of the flattened reduction (k = tap * cin + c in 16-wide steps: lane quad g of step st
+// is k-quad 4 st + g, i.e. tap (4 st + g) / q, channels 4 ((4 st + g) % q) .. +3, so a step can
+// straddle two taps and no channel padding is computed). With KS > 1 the K-slices' partial tiles
+// are summed through LDS in slice order (deterministic).
+template <int NW, int KS>
+__global__ __launch_bounds__(256) void conv3x3_small_kernel(const SmallArgs a) {
+  constexpr int PM = 4 / KS;
+  constexpr int kPixB = 16 * PM;
+  extern __shared__ __attribute__((aligned(16))) float slab[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mi = wave / KS, ks = wave - (wave / KS) * KS;
+  const int p0 = blockIdx.x * kPixB;
+  const int n0 = blockIdx.y * NW * 16;
+  const int HW = a.H * a.W, W2 = a.W + 2;
+  // staged rows: for each image bA..bB the input rows its output rows in [p0, p1] read (+-1)
+  const int p1 = min(p0 + kPixB, a.M) - 1;
+  const int bA = p0 / HW, bB = p1 / HW;
+  const int yA = (p0 - bA * HW) / a.W, yB = (p1 - bB * HW) / a.W;
+  auto ystart = [&](int b) { return b == bA ? yA - 1 : -1; };
+  auto yend = [&](int b) { return b == bB ? yB + 1 : a.H; };  // inclusive
+  int nrows = 0;
+  for (int b = bA; b <= bB; ++b) nrows += yend(b) - ystart(b) + 1;
+
+  // ---- stage: nrows x (W + 2) pixels x cin channels, zero outside the image -------------------
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.in + a.in_co), (short)0, (int)0x7FFFFFF0, 0x00020000);
+  const int Q = a.q;
+  const int total = nrows * W2 * Q;
+  const unsigned qmagic = Q > 1 ? (unsigned)((0x100000000ULL + Q - 1) / Q) : 0u;  // Q == 1: pix = e
+  const unsigned w2magic = (unsigned)((0x100000000ULL + W2 - 1) / W2);
+  // kSU independent loads in flight per thread, then their LDS writes (a rolled load -> write
+  // loop would serialise one memory latency per element)
+  constexpr int kSU = 8;
+  for (int e0 = 0; e0 < total; e0 += 256 * kSU) {
+    f32x4 v[kSU];
+    int dst[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      const int e = e0 + tid + 256 * u;
+      const int pix = Q == 1 ? e : (int)__umulhi((unsigned)e, qmagic);
+      const int c4 = e - pix * Q;
+      const int rs = (int)__umulhi((unsigned)pix, w2magic), xs = pix - rs * W2;
+      int b = bA, r = rs;
+      while (b < bB && r >= yend(b) - ystart(b) + 1) {
+        r -= yend(b) - ystart(b) + 1;
+        ++b;
+      }
+      const int yin = ystart(b) + r, xin = xs - 1;
+      const bool ok = e < total && yin >= 0 && yin < a.H && xin >= 0 && xin < a.W;
+      const unsigned off =
+          ok ? (unsigned)(((((long long)b * a.H + yin) * a.W + xin) * a.in_cs + 4 * c4) * 4) : kOOB;
+      v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
+      dst[u] = e < total ? 4 * (pix * a.pitch + c4) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kSU; ++u)
+      if (dst[u] >= 0) *reinterpret_cast<f32x4*>(slab + dst[u]) = v[u];
+  }
+
+  // ---- this lane's pixel and weight rows ------------------------------------------------------
+  const int fr = lane & 15, g = lane >> 4;
+  const int m = p0 + 16 * mi + fr;
+  int base = 0;  // staged pixel of (b, y, x), the centre tap
+  {
+    const int mm = min(m, a.M - 1);
+    const int b = mm / HW, rr = mm - b * HW;
+    const int y = rr / a.W, x = rr - (rr / a.W) * a.W;
+    int rowslot = 0;
+    for (int bb = bA; bb < b; ++bb) rowslot += yend(bb) - ystart(bb) + 1;
+    rowslot += y - ystart(b);
+    base = rowslot * W2 + x + 1;
+  }
+  const int K = 9 * a.cin;
+  const int KQ = 9 * Q;  // k-quads
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.wt, (short)0, (int)min((long long)a.N * K * 4, (long long)kOOB), 0x00020000);
+  unsigned wrow[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int n = n0 + 16 * j + fr;
+    wrow[j] = n < a.N ? (unsigned)n * (unsigned)K * 4u : kOOB;
+  }
+  f32x4 acc[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  // ---- K loop over this wave's slice of the 16-wide steps --------------------------------------
+  const int nsteps = (KQ + 3) / 4;
+  const int per = (nsteps + KS - 1) / KS;
+  const int s0 = ks * per, s1 = min(nsteps, s0 + per);
+  auto wload = [&](int st, f32x4 (&w)[NW]) {
+    const int kq = 4 * st + g;
+    const bool ok = st < s1 && kq < KQ;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const unsigned off = (ok && wrow[j] != kOOB) ? wrow[j] + (unsigned)kq * 16u : kOOB;
+      w[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsW, off, 0, 0));
+    }
+  };
+  // this lane's (tap, channel quad) at step s0, advanced by 4 quads per step
+  int kq0 = 4 * s0 + g;
+  int tap = kq0 / Q, c4 = kq0 - (kq0 / Q) * Q;
+  f32x4 w1[NW], w2[NW];
+  wload(s0, w1);
+  wload(s0 + 1, w2);
+  for (int st = s0; st < s1; ++st) {
+    f32x4 w[NW];
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      w[j] = w1[j];
+      w1[j] = w2[j];
+    }
+    wload(st + 2, w2);
+    const int ty = tap >= 6 ? 1 : (tap >= 3 ? 0 : -1);
+    const int tx = tap - 3 * (ty + 1) - 1;
+    const bool kok = tap < 9;
+    const int px = kok ? base + ty * W2 + tx : base;
+    f32x4 av = *reinterpret_cast<const f32x4*>(slab + 4 * (px * a.pitch + c4));
+    if (!kok) av = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int j = 0; j < NW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w[j][s2], acc[j], 0, 0, 0);
+    c4 += 4;
+    if (c4 >= Q) {  // Q >= 4: at most one wrap per step... Q in [1, 4) wraps more
+      c4 -= Q;
+      ++tap;
+      while (c4 >= Q) {
+        c4 -= Q;
+        ++tap;
+      }
+    }
+  }
+
+  // ---- K-slice reduction through LDS (slice order: deterministic) ------------------------------
+  if constexpr (KS > 1) {
+    __syncthreads();  // every wave is done reading the slab
+    float* part = slab;
+#pragma unroll
+    for (int j = 0; j < NW; ++j)
+      *reinterpret_cast<f32x4*>(part + ((wave * NW + j) * 64 + lane) * 4) = acc[j];
+    __syncthreads();
+    if (ks != 0) return;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(part + ((wave * NW + j) * 64 + lane) * 4);
+      for (int q2 = 1; q2 < KS; ++q2) v += *reinterpret_cast<const f32x4*>(part + (((wave + q2) * NW + j) * 64 + lane) * 4);
+      acc[j] = v;
+    }
+  }
+
+  // ---- epilogue: acc[j][i] = (pixel 16 mi + 4g + i, channel n0 + 16j + fr) --------------------
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int n = n0 + 16 * j + fr;
+    if (n >= a.n_store) continue;
+    const float sc = a.scale ? a.scale[n] : 1.f;
+    const float bi = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mo = p0 + 16 * mi + 4 * g + i;
+      if (mo >= a.M) continue;
+      float v = acc[j][i] * sc + bi;
+      if (a.res) v += a.res[(size_t)mo * a.res_cs + a.res_co + n];
+      if (a.relu) v = fmaxf(v, 0.f);
+      a.out[(size_t)mo * a.out_cs + a.out_co + n] = v;
+    }
+  }
+}
+
+// LDS floats of the largest slab any block of this problem stages (host mirror of the kernel's
+// row count: the rows of the images a block's pixel range touches, +-1)
+long long slab_floats(int B, int H, int W, int pitch, int pixb) {
+  const long long HW = (long long)H * W, M = (long long)B * HW;
+  long long worst = 0;
+  for (long long p0 = 0; p0 < M; p0 += pixb) {
+    const long long p1 = (p0 + pixb < M ? p0 + pixb : M) - 1;
+    const long long bA = p0 / HW, bB = p1 / HW;
+    const long long yA = (p0 - bA * HW) / W, yB = (p1 - bB * HW) / W;
+    long long rows = 0;
+    for (long long b = bA; b <= bB; ++b) rows += (b == bB ? yB + 1 : H) - (b == bA ? yA - 1 : -1) + 1;
+    if (rows > worst) worst = rows;
+    if (p0 >= (long long)pixb * HW) break;  // block starts repeat modulo lcm(pixb, HW)
+  }
+  return worst * (W + 2) * pitch * 4;
+}
+
+template <int NW, int KS>
+int small_launch(const SmallArgs& a, hipStream_t s) {
+  constexpr int pixb = 64 / KS;
+  long long lds = slab_floats(a.B, a.H, a.W, a.pitch, pixb) * 4;
+  const long long red = 4LL * NW * 64 * 4 * 4;  // K-slice partials
+  if (KS > 1 && lds < red) lds = red;
+  if (lds > 160 * 1024) return KRRN_ESHAPE;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv3x3_small_kernel<NW, KS>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const dim3 grid(krrn_cdiv(a.M, pixb), krrn_cdiv(krrn_cdiv(a.N, 16), NW));
+  hipLaunchKernelGGL((conv3x3_small_kernel<NW, KS>), grid, dim3(256), (size_t)lds, s, a);
+  return krrn_launch_status();
+}
+
+}  // namespace
+
+KRRN_API int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
+                                    const float* wt, int N, int n_store, const float* scale, const float* bias,
+                                    const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
+                                    int relu, int nw, int ks, void* stream) {
+  if (!in || !wt || !out) return KRRN_EARG;
+  if (B < 1 || H < 1 || W < 1 || N < 1 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
+  if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(in) || !krrn_aligned16(wt)) return KRRN_EALIGN;
+  if (out_co + n_store > out_cs || (res && res_co + n_store > res_cs)) return KRRN_ESHAPE;
+  if (nw < 1 || nw > 3 || (ks != 1 && ks != 2 && ks != 4)) return KRRN_EARG;
+  const long long M = (long long)B * H * W;
+  if (M > 0x7fffffffLL || M * in_cs * 4 >= 0x7FFFFFF0LL || (long long)N * 9 * cin * 4 >= (long long)kOOB)
+    return KRRN_ESHAPE;
+  SmallArgs a;
+  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = H; a.W = W; a.cin = cin;
+  a.wt = wt; a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
+  a.res = res; a.res_cs = res_cs; a.res_co = res_co; a.out = out; a.out_cs = out_cs; a.out_co = out_co;
+  a.relu = relu; a.M = (int)M;
+  a.q = cin / 4;
+  a.pitch = a.q | 1;
+  hipStream_t s = (hipStream_t)stream;
+#define KRRN_SMALL(NWV, KSV) \
+  if (nw == NWV && ks == KSV) return small_launch<NWV, KSV>(a, s);
+  KRRN_SMALL(1, 1) KRRN_SMALL(2, 1) KRRN_SMALL(3, 1)
+  KRRN_SMALL(1, 2) KRRN_SMALL(2, 2) KRRN_SMALL(3, 2)
+  KRRN_SMALL(1, 4) KRRN_SMALL(2, 4) KRRN_SMALL(3, 4)
+#undef KRRN_SMALL
+  return KRRN_EARG;
+}

@@ -40,6 +40,8 @@ DECONV_FOLD = os.environ.get("KRRN_DECONV_FOLD", "1") == "1"
 # transposed convs (4 parity-class convs) as one grouped launch
 CONVT_GROUP = os.environ.get("KRRN_CONVT_GROUP", "1") == "1"
 CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
+# narrow 3x3 stride-1 convs (the HRNet branches' BasicBlocks) on the LDS-staged direct kernel
+SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
 
 BN_MOMENTUM = 0.1
 
@@ -222,9 +224,24 @@ class _Builder:
             U = ops.wino_weights(conv, self.dev, cin_map=cin_map, cin_p=x.cp)
             self.specs.append(U)
             self.emit_wino(x, spec, U, out, res, relu)
+        elif SMALL_CONV and ops.small_conv_eligible(spec, x):
+            self.emit_small(x, spec, out, res, relu)
         else:
             self.emit_conv(x, spec, out, res, relu)
         return out
+
+    def emit_small(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
+        np_ = pad4(spec.cout)
+        M = x.B * out.H * out.W
+        ntiles = (np_ + 15) // 16
+        nw, ks = ops.small_conv_config(M, ntiles, spec.cin_p)
+        self.plan.add("krrn_conv3x3_small_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(spec.wt[0]), np_,
+                      np_, ptr(spec.scale), ptr(spec.bias), ptr(res.t) if res is not None else ptr(None),
+                      res.cs if res is not None else 0, res.co if res is not None else 0, ptr(out.t), out.cs, out.co,
+                      int(relu), nw, ks,
+                      meta=dict(kernel=f"conv3x3_small<{nw},{ks}>", flops=2.0 * spec.cin * spec.cout * 9 * M, tag=tag,
+                                M=M, N=np_, K=spec.cin_p * 9, splits=1,
+                                mfma_flops=2.0 * 16 * ((9 * spec.cin_p // 4 + 3) // 4) * 16 * ntiles * M))
 
     def emit_wino(self, x: Act, spec, U: torch.Tensor, out: Act, res: Optional[Act], relu: bool,
                   tag: str = "conv"):

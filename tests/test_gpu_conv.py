@@ -222,3 +222,37 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     assert torch.count_nonzero(outs[0][..., np_:]).item() == 0
     # the three kernels are bit-identical (same V operands and MFMA order), every output written
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("B,cin,cout,H,W,co,nw,ks", [(3, 20, 18, 30, 30, 0, 2, 1), (64, 144, 144, 4, 4, 0, 1, 4),
+                                                     (8, 36, 36, 15, 15, 4, 3, 2), (5, 72, 72, 8, 8, 0, 1, 4),
+                                                     (2, 12, 40, 7, 9, 0, 2, 2), (3, 4, 8, 5, 6, 0, 1, 1)])
+def test_conv3x3_small(dev, B, cin, cout, H, W, co, nw, ks):
+    """LDS-staged direct 3x3 conv (the HRNet branch BasicBlock convs): blocks spanning several
+    images / rows, channel-offset input, residual + ReLU, partial 16-channel tiles, vs torch fp32."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, ptr
+    g = torch.Generator().manual_seed(cin * cout + H)
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, W, generator=g)
+    res = torch.randn(B, cout, H, W, generator=g)
+    ref = torch.relu(bn(conv(x)) + res).detach()
+    cs = ops.pad4(cin) + co + 4
+    xa = _nhwc(x, dev, cs=cs, co=co)
+    spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
+    ra = _nhwc(res, dev)
+    np_ = ops.pad4(cout)
+    out = ops.new_act(B, H, W, cout, dev, cs=np_ + 4)
+    out.t.fill_(float("nan"))
+    out.t[..., np_:] = 0.0
+    _lib.check(_lib.lib().krrn_conv3x3_small_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(spec.wt[0]), np_,
+                                                 np_, ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
+                                                 out.cs, 0, 1, nw, ks, P(torch.cuda.current_stream().cuda_stream)),
+               "small conv")
+    torch.cuda.synchronize()
+    got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, **TOL)
+    assert torch.count_nonzero(out.t[..., np_:]).item() == 0
