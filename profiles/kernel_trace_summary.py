@@ -16,6 +16,8 @@ from collections import defaultdict
 
 
 def short(name):
+    if name.startswith("Cijk"):
+        return "hipblaslt_gemm_f32"
     m = re.search(r"(conv_gemm_f32_kernel<[^>]*>|splitk_epilogue_kernel|\w+_kernel(<[^>]*>)?|__amd_\w+)", name)
     return m.group(1) if m else name[:60]
 
@@ -23,7 +25,8 @@ def short(name):
 def main(path, out=None):
     rows = list(csv.DictReader(open(path)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), int(r["Queue_Id"]))
-                 for r in rows if "anonymous namespace" in r["Kernel_Name"]), key=lambda x: x[0])
+                 for r in rows if "anonymous namespace" in r["Kernel_Name"] or r["Kernel_Name"].startswith("Cijk")),
+                key=lambda x: x[0])
     # mark kernels that overlap any other kernel (by more than TOL ns: back-to-back kernels of
     # one stream can show sub-microsecond timestamp overlap on a fast box)
     TOL = 2000

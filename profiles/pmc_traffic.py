@@ -21,8 +21,13 @@ def _short(name: str) -> str:
     m = re.search(r"conv_group_kernel<(\d+), (\d+), (\d+), \d+>", name)
     if m:
         return f"conv_group<{m.group(1)},{m.group(2)},{m.group(3)}>"
-    if "wino_f23_kernel" in name:
+    if "wino_f23" in name:
         return "wino_f23<32,32,16>"
+    m = re.search(r"conv3x3_small_kernel<(\d+), (\d+)>", name)
+    if m:
+        return f"conv3x3_small<{m.group(1)},{m.group(2)}>"
+    if name.startswith("Cijk"):
+        return "hipblaslt_gemm_f32"
     m = re.search(r"(\w+_kernel)", name)
     return m.group(1) if m else name
 
