@@ -126,6 +126,23 @@ int krrn_wino_variant(int v);
 int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* wt,
                            int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                            int res_co, float* out, int out_cs, int out_co, int relu, int nw, int ks, void* stream);
+/* The arguments of krrn_conv3x3_small_f32 as a struct, and up to 4 independent such convs in ONE
+ * launch (the j-th BasicBlock conv of every HRNet branch, myhrnet.py:177-231: the branches are
+ * independent until the fuse layer). Each problem computes exactly what krrn_conv3x3_small_f32
+ * computes with the same arguments (bit-identical). */
+typedef struct krrn_small_desc {
+  const float* in;
+  int in_cs, in_co, B, H, W, cin;
+  const float* wt;
+  int N, n_store;
+  const float* scale;
+  const float* bias;
+  const float* res;
+  int res_cs, res_co;
+  float* out;
+  int out_cs, out_co, relu, nw, ks;
+} krrn_small_desc;
+int krrn_conv3x3_small_group_f32(const krrn_small_desc* descs, int n, void* stream);
 
 /* k nearest neighbours without the [n, n] distance matrix.
  * Replaces gcn3d.get_neighbor_index (gcn3d.py:15-26; mode 0, drop_first = 1: topk(k+1)[1:])
@@ -207,17 +224,20 @@ int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const float* w4, co
                         float* pred_t, float* t_res, void* stream);
 
 /* Batched PnP-RANSAC: Trainer.get_pose (tools/trainer.py:383-438), cv2.solvePnPRansac(EPNP,
- * reprojectionError = thr, confidence 0.9999) restated: one workgroup per crop.
+ * reprojectionError = thr, confidence = conf (0.9999 there), iterationsCount = H) restated.
  * xyz [B][3][HW] (normalised model coords), choose int64 [B][N], sel int32 [B][P] (the
  * randperm(N)[:P] subset), x/ymap [B][N] full-frame pixels, K4 [B][4] = fx fy cx cy,
- * extent / lfborder f64 [B][3], subsets int32 [B][H][5]; workspace: B*H*13 floats (per-hypothesis
- * pose + inlier count). Outputs R [B][9] row-major, t [B][3], inlier count [B] (0 = RANSAC failed
- * -> R = I, t = 0), inlier_mask [B][P] (optional). Two launches: hypotheses spread over
- * (crop, 16-hypothesis) workgroups, then one wave per crop for selection + EPnP refinement. */
+ * extent / lfborder f64 [B][3], subsets int32 [B][H][5] (hypothesis h's sample); workspace:
+ * B*H*13 floats (per-hypothesis pose + inlier count). Hypotheses are scored in parallel; the
+ * selection is ptsetreg.cpp's loop over them in order with its adaptive iteration count
+ * (niters <- RANSACUpdateNumIters(conf, outlier ratio, 5, niters) on every new best). Outputs R
+ * [B][9] row-major, t [B][3], inlier count [B] (0 = RANSAC failed -> R = I, t = 0), inlier_mask
+ * [B][P] (optional). Two launches: one 16-lane group per hypothesis, then one wave per crop for
+ * the selection + EPnP on all inliers. */
 int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choose, int N, const int* sel, int P,
                         const float* xmap, const float* ymap, const float* K4, const double* extent,
-                        const double* lfborder, const int* subsets, int H, float thr, float* workspace, float* R,
-                        float* t, int* inliers, unsigned char* inlier_mask, int B, void* stream);
+                        const double* lfborder, const int* subsets, int H, float thr, float conf, float* workspace,
+                        float* R, float* t, int* inliers, unsigned char* inlier_mask, int B, void* stream);
 
 /* torch.randperm(n)[:k] per row (gcn3d.py:239, trainer.py:407) from a counter-based generator
  * seeded by *seed_ptr (device memory) and `stream_id`; n <= 4096. out int32 [rows][k]. */

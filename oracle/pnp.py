@@ -26,8 +26,8 @@ def _load():
         _lib.oracle_epnp.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] + [ctypes.c_void_p] * 3
         _lib.oracle_pnp_ransac.restype = ctypes.c_int
         _lib.oracle_pnp_ransac.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
-                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
-                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 
 
@@ -46,8 +46,9 @@ def epnp(pw, uv, K4):
     return R.reshape(3, 3), t, err
 
 
-def pnp_ransac(obj, img, K4, subsets, thr=1.0):
-    """One crop: obj [P,3] f32, img [P,2] f32, K4 (fx, fy, cx, cy), subsets [H,5] int.
+def pnp_ransac(obj, img, K4, subsets, thr=1.0, conf=0.9999):
+    """One crop: obj [P,3] f32, img [P,2] f32, K4 (fx, fy, cx, cy), subsets [H,5] int (H =
+    iterationsCount; the loop stops early at cv2's adaptive count for `conf`).
 
     Returns (R [3,3] f32, t [3] f32, inlier_count, inlier_mask [P] bool, best_h)."""
     obj = np.ascontiguousarray(obj, dtype=np.float32)
@@ -59,7 +60,7 @@ def pnp_ransac(obj, img, K4, subsets, thr=1.0):
     mask = np.zeros(len(obj), np.uint8)
     best = ctypes.c_int(-1)
     cnt = _load().oracle_pnp_ransac(_p(obj), _p(img), len(obj), _p(K4), _p(subsets), len(subsets), float(thr),
-                                    _p(R), _p(t), _p(mask), ctypes.byref(best))
+                                    float(conf), _p(R), _p(t), _p(mask), ctypes.byref(best))
     return R.reshape(3, 3), t, cnt, mask.astype(bool), best.value
 
 

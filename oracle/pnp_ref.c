@@ -12,13 +12,14 @@
  *     PCA control points, barycentric alphas, M (2n x 12), null space of M^T M (4 smallest
  *     eigenvectors), L_6x10 / rho, beta approximations 1/2/3 each refined by 5 Gauss-Newton
  *     steps, R,t by Procrustes, the solution with the smallest mean reprojection error wins;
- *   - RANSAC with 5-point EPnP hypotheses, inlier test ||proj - img||^2 <= thr^2, best =
- *     most inliers (first hypothesis wins ties, accepted only with >= 5 inliers, as
- *     ptsetreg.cpp's `goodCount > max(maxGoodCount, modelPoints - 1)`), then EPnP on all
- *     inliers of the best hypothesis.
+ *   - RANSAC as ptsetreg.cpp runs it: 5-point EPnP hypotheses in order while h < niters,
+ *     inlier test ||proj - img||^2 <= thr^2, a count above max(best, modelPoints - 1) becomes
+ *     the best and sets niters = RANSACUpdateNumIters(confidence, outlier ratio, 5, niters)
+ *     (iterationsCount = H), then EPnP on all inliers of the best hypothesis.
  * Deliberate, documented differences (DESIGN.md "PnP"): the H hypothesis subsets are given
- * by the caller (so GPU and oracle score identical subsets) instead of cv::RNG with
- * adaptive early exit; Procrustes uses the Kabsch det-correction R = U diag(1,1,d) V^T.
+ * by the caller (so GPU and oracle score identical subsets) instead of cv::RNG; the 12x12
+ * solve is the GPU kernel's parallel-ordered Jacobi (jacobi12_par); Procrustes uses the Kabsch
+ * det-correction R = U diag(1,1,d) V^T.
  * PARITY UNPINNED against cv2 itself (not installable here); pinned by known-answer tests
  * (exact recovery of a known (R, t) on noiseless correspondences, tests/test_oracle_pnp.py).
  */
@@ -83,6 +84,105 @@ static void jacobi_eig(double* A, int n, double* w, double* V) {
   }
   memcpy(w, ws, sizeof(double) * n);
   memcpy(V, Vt, sizeof(double) * n * n);
+}
+
+/* The 12x12 solve of EPnP (M^T M) exactly as csrc/pnp.hip's eig12_group evaluates it:
+ * parallel-ordered (round-robin) Jacobi, 11 steps of 6 disjoint rotations per sweep; per step every
+ * pair's (c, s) from the pre-step matrix, then A <- A J, A <- J^T A, U <- U J. Convergence
+ * off <= 1e-30 tot with per-row sums reduced by the kernel's 16-lane butterfly. Returns the
+ * eigenvectors of the 4 smallest eigenvalues, ascending (ties: lower column first): v4[q][k]. */
+static double bfly16(const double* x) {
+  double v[16], t[16];
+  for (int i = 0; i < 16; ++i) v[i] = x[i];
+  for (int off = 8; off > 0; off >>= 1) {
+    for (int i = 0; i < 16; ++i) t[i] = v[i] + v[i ^ off];
+    for (int i = 0; i < 16; ++i) v[i] = t[i];
+  }
+  return v[0];
+}
+
+static int rr_partner(int k, int r) { return r == 11 ? k : (r == k ? 11 : (2 * k - r + 11) % 11); }
+
+static void jacobi12_par(double* A, double v4[4][12]) {
+  double U[144], A0[144];
+  for (int i = 0; i < 144; ++i) U[i] = (i % 13 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double tr[16] = {0}, orr[16] = {0};
+    for (int r = 0; r < 12; ++r)
+      for (int j = 0; j < 12; ++j) {
+        const double x2 = A[r * 12 + j] * A[r * 12 + j];
+        tr[r] += x2;
+        if (j != r) orr[r] += x2;
+      }
+    const double tot = bfly16(tr), off = bfly16(orr);
+    if (off <= 1e-30 * tot || off < 1e-300) break;
+    for (int k = 0; k < 11; ++k) {
+      double c[12], sn[12];
+      for (int r = 0; r < 12; ++r) {
+        const int pr = rr_partner(k, r), lo = r < pr ? r : pr, hi = r < pr ? pr : r;
+        const double apq = A[lo * 12 + hi], app = A[lo * 13], aqq = A[hi * 13];
+        c[r] = 1.0;
+        sn[r] = 0.0;
+        if (!(fabs(apq) < 1e-300 || fabs(apq) < 1e-18 * sqrt(fabs(app * aqq)))) {
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          c[r] = 1.0 / sqrt(tt * tt + 1.0);
+          sn[r] = tt * c[r];
+        }
+      }
+      int pp[6], qq[6];
+      for (int i = 0; i < 6; ++i) {
+        const int x = i == 0 ? k : (k + i) % 11, y = i == 0 ? 11 : (k - i + 11) % 11;
+        pp[i] = x < y ? x : y;
+        qq[i] = x < y ? y : x;
+      }
+      for (int r = 0; r < 12; ++r)
+        for (int i = 0; i < 6; ++i) {
+          const double cs = c[pp[i]], ss = sn[pp[i]];
+          const double xp = A[r * 12 + pp[i]], xq = A[r * 12 + qq[i]];
+          A[r * 12 + pp[i]] = cs * xp - ss * xq;
+          A[r * 12 + qq[i]] = ss * xp + cs * xq;
+        }
+      memcpy(A0, A, sizeof A0);
+      for (int r = 0; r < 12; ++r) {
+        const int pr = rr_partner(k, r);
+        for (int j = 0; j < 12; ++j) {
+          const double y = A0[pr * 12 + j], x = A0[r * 12 + j];
+          A[r * 12 + j] = r < pr ? c[r] * x - sn[r] * y : sn[r] * y + c[r] * x;
+        }
+      }
+      for (int r = 0; r < 12; ++r)
+        for (int i = 0; i < 6; ++i) {
+          const double cs = c[pp[i]], ss = sn[pp[i]];
+          const double xp = U[r * 12 + pp[i]], xq = U[r * 12 + qq[i]];
+          U[r * 12 + pp[i]] = cs * xp - ss * xq;
+          U[r * 12 + qq[i]] = ss * xp + cs * xq;
+        }
+    }
+  }
+  unsigned used = 0;
+  for (int q = 0; q < 4; ++q) {
+    int m = -1;
+    double wm = 0.0;
+    for (int j = 0; j < 12; ++j) {
+      if (used & (1u << j)) continue;
+      if (m < 0 || A[j * 13] < wm) { m = j; wm = A[j * 13]; }
+    }
+    used |= 1u << m;
+    for (int k = 0; k < 12; ++k) v4[q][k] = U[k * 12 + m];
+  }
+}
+
+/* cv::RANSACUpdateNumIters (ptsetreg.cpp) */
+static int ransac_update_niters(double conf, double ep, int model_points, int max_iters) {
+  conf = fmin(fmax(conf, 0.0), 1.0);
+  ep = fmin(fmax(ep, 0.0), 1.0);
+  double num = fmax(1.0 - conf, 2.2250738585072014e-308);
+  double denom = 1.0 - pow(1.0 - ep, (double)model_points);
+  if (denom < 2.2250738585072014e-308) return 0;
+  num = log(num);
+  denom = log(denom);
+  return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
 }
 
 /* least squares min ||A x - b|| for A m x n (m <= 6, n <= 5) via the pseudo-inverse built
@@ -288,8 +388,10 @@ static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R
     for (int i = 0; i < 12; ++i)
       for (int j = 0; j < 12; ++j) MtM[i * 12 + j] += r1[i] * r1[j] + r2[i] * r2[j];
   }
-  double w[12], ut[144];
-  jacobi_eig(MtM, 12, w, ut);
+  double v4[4][12], ut[144];
+  jacobi12_par(MtM, v4);
+  for (int q = 0; q < 4; ++q)
+    for (int k = 0; k < 12; ++k) ut[(11 - q) * 12 + k] = v4[q][k];  /* rows 11, 10, 9, 8: ascending */
   /* L_6x10 and rho */
   double L[60], rho[6];
   {
@@ -436,14 +538,15 @@ void oracle_pnp_hypotheses(const float* obj, const float* img, int P, const floa
  * hypothesis, and returns the inlier count of the best hypothesis (0 = RANSAC failed).
  */
 int oracle_pnp_ransac(const float* obj, const float* img, int P, const float* K4, const int* subsets, int H,
-                      float thr, float* R_out, float* t_out, unsigned char* inlier_mask, int* best_h) {
+                      float thr, float conf, float* R_out, float* t_out, unsigned char* inlier_mask, int* best_h) {
   static double pw[3 * MAXP], uv[2 * MAXP];
   Cam cam = {K4[0], K4[1], K4[2], K4[3]};
   if (P > MAXP) P = MAXP;
   int best = -1, best_cnt = 0;
   double bestR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, bestt[3] = {0, 0, 0};
   const float thr2 = thr * thr;
-  for (int h = 0; h < H; ++h) {
+  int niters = H;
+  for (int h = 0; h < niters; ++h) {
     double spw[15], suv[10], R[9], t[3];
     for (int i = 0; i < 5; ++i) {
       const int id = subsets[5 * h + i];
@@ -462,11 +565,13 @@ int oracle_pnp_ransac(const float* obj, const float* img, int P, const float* K4
       const float dv = img[2 * p + 1] - ((float)cam.fv * yc * iz + (float)cam.vc);
       if (du * du + dv * dv <= thr2) ++cnt;
     }
+    /* ptsetreg.cpp: goodCount > max(maxGoodCount, modelPoints - 1), then the adaptive count */
     if (cnt > (best_cnt > 4 ? best_cnt : 4)) {
       best_cnt = cnt;
       best = h;
       memcpy(bestR, R, sizeof bestR);
       memcpy(bestt, t, sizeof bestt);
+      niters = ransac_update_niters((double)conf, (double)(P - cnt) / P, 5, niters);
     }
   }
   if (best_h) *best_h = best;

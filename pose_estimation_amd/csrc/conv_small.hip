@@ -51,14 +51,13 @@ constexpr unsigned kOOB = 0xFFFFFFF0u;
 // straddle two taps and no channel padding is computed). With KS > 1 the K-slices' partial tiles
 // are summed through LDS in slice order (deterministic).
 template <int NW, int KS>
-__global__ __launch_bounds__(256) void conv3x3_small_kernel(const SmallArgs a) {
+__device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, float* slab) {
   constexpr int PM = 4 / KS;
   constexpr int kPixB = 16 * PM;
-  extern __shared__ __attribute__((aligned(16))) float slab[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mi = wave / KS, ks = wave - (wave / KS) * KS;
-  const int p0 = blockIdx.x * kPixB;
-  const int n0 = blockIdx.y * NW * 16;
+  const int p0 = bx * kPixB;
+  const int n0 = by * NW * 16;
   const int HW = a.H * a.W, W2 = a.W + 2;
   // staged rows: for each image bA..bB the input rows its output rows in [p0, p1] read (+-1)
   const int p1 = min(p0 + kPixB, a.M) - 1;
@@ -149,34 +148,41 @@ __global__ __launch_bounds__(256) void conv3x3_small_kernel(const SmallArgs a) {
   // this lane's (tap, channel quad) at step s0, advanced by 4 quads per step
   int kq0 = 4 * s0 + g;
   int tap = kq0 / Q, c4 = kq0 - (kq0 / Q) * Q;
-  f32x4 w1[NW], w2[NW];
-  wload(s0, w1);
-  wload(s0 + 1, w2);
-  for (int st = s0; st < s1; ++st) {
-    f32x4 w[NW];
+#ifndef KRRN_SMALL_PF
+#define KRRN_SMALL_PF 2
+#endif
+  // weights KRRN_SMALL_PF steps ahead in a register ring (slot u of every PF-step group)
+  constexpr int PF = KRRN_SMALL_PF;
+  f32x4 wr[PF][NW];
 #pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      w[j] = w1[j];
-      w1[j] = w2[j];
-    }
-    wload(st + 2, w2);
-    const int ty = tap >= 6 ? 1 : (tap >= 3 ? 0 : -1);
-    const int tx = tap - 3 * (ty + 1) - 1;
-    const bool kok = tap < 9;
-    const int px = kok ? base + ty * W2 + tx : base;
-    f32x4 av = *reinterpret_cast<const f32x4*>(slab + 4 * (px * a.pitch + c4));
-    if (!kok) av = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < PF; ++u) wload(s0 + u, wr[u]);
+  for (int st0 = s0; st0 < s1; st0 += PF) {
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2)
+    for (int u = 0; u < PF; ++u) {
+      const int st = st0 + u;
+      if (st >= s1) break;
+      f32x4 w[NW];
 #pragma unroll
-      for (int j = 0; j < NW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w[j][s2], acc[j], 0, 0, 0);
-    c4 += 4;
-    if (c4 >= Q) {  // Q >= 4: at most one wrap per step... Q in [1, 4) wraps more
-      c4 -= Q;
-      ++tap;
-      while (c4 >= Q) {
+      for (int j = 0; j < NW; ++j) w[j] = wr[u][j];
+      wload(st + PF, wr[u]);
+      const int ty = tap >= 6 ? 1 : (tap >= 3 ? 0 : -1);
+      const int tx = tap - 3 * (ty + 1) - 1;
+      const bool kok = tap < 9;
+      const int px = kok ? base + ty * W2 + tx : base;
+      f32x4 av = *reinterpret_cast<const f32x4*>(slab + 4 * (px * a.pitch + c4));
+      if (!kok) av = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int j = 0; j < NW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w[j][s2], acc[j], 0, 0, 0);
+      c4 += 4;
+      if (c4 >= Q) {  // Q >= 4: at most one wrap per step... Q in [1, 4) wraps more
         c4 -= Q;
         ++tap;
+        while (c4 >= Q) {
+          c4 -= Q;
+          ++tap;
+        }
       }
     }
   }
@@ -217,6 +223,45 @@ __global__ __launch_bounds__(256) void conv3x3_small_kernel(const SmallArgs a) {
   }
 }
 
+template <int NW, int KS>
+__global__ __launch_bounds__(256) void conv3x3_small_kernel(const SmallArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float slab[];
+  small_body<NW, KS>(a, blockIdx.x, blockIdx.y, slab);
+}
+
+// Up to 4 independent problems (the j-th BasicBlock conv of every HRNet branch) in one launch:
+// block b belongs to the problem whose [start, start + blocks) range holds it, and runs that
+// problem's (NW, KS) body on its (m-block, n-block) exactly as the single launch would (the
+// same instructions per output: bit-identical results). Problems are ordered longest block first.
+constexpr int kSmallMaxGroup = 4;
+struct SmallGroup {
+  SmallArgs a[kSmallMaxGroup];
+  int cfg[kSmallMaxGroup];  // (nw - 1) + 3 * log2(ks)
+  int gx[kSmallMaxGroup];   // m-blocks
+  int start[kSmallMaxGroup + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void conv3x3_small_group_kernel(const SmallGroup g) {
+  extern __shared__ __attribute__((aligned(16))) float slab[];
+  const int blk = blockIdx.x;
+  int i = 0;
+  while (i + 1 < g.n && blk >= g.start[i + 1]) ++i;
+  const int r = blk - g.start[i];
+  const int by = r / g.gx[i], bx = r - by * g.gx[i];
+  switch (g.cfg[i]) {
+    case 0: small_body<1, 1>(g.a[i], bx, by, slab); break;
+    case 1: small_body<2, 1>(g.a[i], bx, by, slab); break;
+    case 2: small_body<3, 1>(g.a[i], bx, by, slab); break;
+    case 3: small_body<1, 2>(g.a[i], bx, by, slab); break;
+    case 4: small_body<2, 2>(g.a[i], bx, by, slab); break;
+    case 5: small_body<3, 2>(g.a[i], bx, by, slab); break;
+    case 6: small_body<1, 4>(g.a[i], bx, by, slab); break;
+    case 7: small_body<2, 4>(g.a[i], bx, by, slab); break;
+    default: small_body<3, 4>(g.a[i], bx, by, slab); break;
+  }
+}
+
 // LDS floats of the largest slab any block of this problem stages (host mirror of the kernel's
 // row count: the rows of the images a block's pixel range touches, +-1)
 long long slab_floats(int B, int H, int W, int pitch, int pixb) {
@@ -234,29 +279,37 @@ long long slab_floats(int B, int H, int W, int pitch, int pixb) {
   return worst * (W + 2) * pitch * 4;
 }
 
+// dynamic LDS bytes of one (NW, KS) launch: the slab, or the K-slice partials if larger
+long long small_lds(const SmallArgs& a, int nw, int ks) {
+  long long lds = slab_floats(a.B, a.H, a.W, a.pitch, 64 / ks) * 4;
+  const long long red = 4LL * nw * 64 * 4 * 4;
+  if (ks > 1 && lds < red) lds = red;
+  return lds;
+}
+
+int set_lds(const void* fn, long long lds) {
+  if (lds > 160 * 1024) return KRRN_ESHAPE;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  return KRRN_OK;
+}
+
 template <int NW, int KS>
 int small_launch(const SmallArgs& a, hipStream_t s) {
   constexpr int pixb = 64 / KS;
-  long long lds = slab_floats(a.B, a.H, a.W, a.pitch, pixb) * 4;
-  const long long red = 4LL * NW * 64 * 4 * 4;  // K-slice partials
-  if (KS > 1 && lds < red) lds = red;
-  if (lds > 160 * 1024) return KRRN_ESHAPE;
-  if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv3x3_small_kernel<NW, KS>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-  }
+  const long long lds = small_lds(a, NW, KS);
+  const int st = set_lds((const void*)conv3x3_small_kernel<NW, KS>, lds);
+  if (st != KRRN_OK) return st;
   const dim3 grid(krrn_cdiv(a.M, pixb), krrn_cdiv(krrn_cdiv(a.N, 16), NW));
   hipLaunchKernelGGL((conv3x3_small_kernel<NW, KS>), grid, dim3(256), (size_t)lds, s, a);
   return krrn_launch_status();
 }
 
-}  // namespace
-
-KRRN_API int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
-                                    const float* wt, int N, int n_store, const float* scale, const float* bias,
-                                    const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
-                                    int relu, int nw, int ks, void* stream) {
+int make_args(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* wt, int N,
+              int n_store, const float* scale, const float* bias, const float* res, int res_cs, int res_co,
+              float* out, int out_cs, int out_co, int relu, int nw, int ks, SmallArgs& a) {
   if (!in || !wt || !out) return KRRN_EARG;
   if (B < 1 || H < 1 || W < 1 || N < 1 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
   if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
@@ -266,13 +319,25 @@ KRRN_API int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B
   const long long M = (long long)B * H * W;
   if (M > 0x7fffffffLL || M * in_cs * 4 >= 0x7FFFFFF0LL || (long long)N * 9 * cin * 4 >= (long long)kOOB)
     return KRRN_ESHAPE;
-  SmallArgs a;
   a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = H; a.W = W; a.cin = cin;
   a.wt = wt; a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
   a.res = res; a.res_cs = res_cs; a.res_co = res_co; a.out = out; a.out_cs = out_cs; a.out_co = out_co;
   a.relu = relu; a.M = (int)M;
   a.q = cin / 4;
   a.pitch = a.q | 1;
+  return KRRN_OK;
+}
+
+}  // namespace
+
+KRRN_API int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
+                                    const float* wt, int N, int n_store, const float* scale, const float* bias,
+                                    const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
+                                    int relu, int nw, int ks, void* stream) {
+  SmallArgs a;
+  const int st = make_args(in, in_cs, in_co, B, H, W, cin, wt, N, n_store, scale, bias, res, res_cs, res_co, out,
+                           out_cs, out_co, relu, nw, ks, a);
+  if (st != KRRN_OK) return st;
   hipStream_t s = (hipStream_t)stream;
 #define KRRN_SMALL(NWV, KSV) \
   if (nw == NWV && ks == KSV) return small_launch<NWV, KSV>(a, s);
@@ -281,4 +346,48 @@ KRRN_API int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B
   KRRN_SMALL(1, 4) KRRN_SMALL(2, 4) KRRN_SMALL(3, 4)
 #undef KRRN_SMALL
   return KRRN_EARG;
+}
+
+KRRN_API int krrn_conv3x3_small_group_f32(const krrn_small_desc* d, int n, void* stream) {
+  if (!d || n < 1 || n > kSmallMaxGroup) return KRRN_EARG;
+  SmallGroup g;
+  long long blocks[kSmallMaxGroup], lds = 0;
+  int order[kSmallMaxGroup];
+  for (int i = 0; i < n; ++i) {
+    SmallArgs& a = g.a[i];
+    const krrn_small_desc& q = d[i];
+    const int st = make_args(q.in, q.in_cs, q.in_co, q.B, q.H, q.W, q.cin, q.wt, q.N, q.n_store, q.scale, q.bias,
+                             q.res, q.res_cs, q.res_co, q.out, q.out_cs, q.out_co, q.relu, q.nw, q.ks, a);
+    if (st != KRRN_OK) return st;
+    const long long l = small_lds(a, q.nw, q.ks);
+    if (l > lds) lds = l;
+    order[i] = i;
+  }
+  // longest block first: per-block MFMA steps ~ ceil(9 cin / 16) / ks x nw tiles
+  auto cost = [&](int i) { return (long long)((9 * d[i].cin + 15) / 16 + d[i].ks - 1) / d[i].ks * d[i].nw; };
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && cost(order[j]) > cost(order[j - 1]); --j) {
+      const int t = order[j];
+      order[j] = order[j - 1];
+      order[j - 1] = t;
+    }
+  SmallGroup h;
+  h.n = n;
+  long long total = 0;
+  for (int r = 0; r < n; ++r) {
+    const int i = order[r];
+    const krrn_small_desc& q = d[i];
+    h.a[r] = g.a[i];
+    h.cfg[r] = (q.nw - 1) + 3 * (q.ks == 1 ? 0 : (q.ks == 2 ? 1 : 2));
+    h.gx[r] = krrn_cdiv(g.a[i].M, 64 / q.ks);
+    blocks[r] = (long long)h.gx[r] * krrn_cdiv(krrn_cdiv(q.N, 16), q.nw);
+    h.start[r] = (int)total;
+    total += blocks[r];
+  }
+  h.start[n] = (int)total;
+  if (total > 0x7fffffffLL) return KRRN_ESHAPE;
+  const int st = set_lds((const void*)conv3x3_small_group_kernel, lds);
+  if (st != KRRN_OK) return st;
+  hipLaunchKernelGGL(conv3x3_small_group_kernel, dim3((unsigned)total), dim3(256), (size_t)lds, (hipStream_t)stream, h);
+  return krrn_launch_status();
 }

@@ -1,23 +1,25 @@
-// Batched PnP-RANSAC for Trainer.get_pose (tools/trainer.py:383-438).
+// Batched PnP-RANSAC for Trainer.get_pose (tools/trainer.py:383-438):
+//   cv2.solvePnPRansac(obj, img, K, None, flags=SOLVEPNP_EPNP, confidence=0.9999, reprojectionError=1)
 //
 //   obj[i] = float( xyz[b, :, choose[b, sel[b, i]]] * extent[b] + lfborder[b] )   (f64 math, then
 //            f32 like cv::solvePnPRansac's CV_32F conversion of objectPoints)
 //   img[i] = (x_map_choosed[b, sel[b, i]], y_map_choosed[b, sel[b, i]])
-//   H hypotheses: EPnP on 5 correspondences each (one thread per hypothesis, f64),
-//   score: #{ i : ||proj(R_h, t_h, obj_i) - img_i||^2 <= thr^2 } (f32, FMA-free, the same
-//   expression as oracle/pnp_ref.c), best = most inliers / lowest h, accepted with >= 5
-//   inliers (ptsetreg.cpp: goodCount > max(maxGoodCount, modelPoints - 1)),
+//   H hypotheses: EPnP on 5 correspondences each (f64), scored in parallel:
+//   #{ i : ||proj(R_h, t_h, obj_i) - img_i||^2 <= thr^2 } (f32, FMA-free, the same expression as
+//   oracle/pnp_ref.c); selection = ptsetreg.cpp's sequential loop over h < niters: a count above
+//   max(best, modelPoints - 1) becomes the best and sets niters = RANSACUpdateNumIters(conf,
+//   outlier ratio, 5, niters) (cv2's adaptive early exit, iterationsCount = H = 100);
 //   refine: EPnP on every inlier of the best hypothesis; R as a rotation matrix (the
 //   reference's Rodrigues round trip rvec -> kornia R is the identity map on R).
 // Subsets come from the caller (krrn_ransac_subsets or explicit test inputs) so the GPU and
 // the CPU oracle score identical hypotheses.
 //
-// Latency design: a 5-point EPnP is ~100 small dense solves. Every 3x3 / 4x4 / 5x5 symmetric
-// eigen-solve is a fully unrolled cyclic Jacobi whose indices are all compile-time constants,
-// so the matrices live in VGPRs; the one 12x12 solve (M^T M) runs on a per-thread LDS arena
-// with runtime (p, q) but unrolled rows, so each rotation issues its loads back to back.
-// (A dynamically indexed private array lives in scratch: the first version spent 2.8 ms per
-// 64-crop batch there.)
+// Latency design: a 5-point EPnP is a chain of small dense f64 solves. Every 3x3 / 4x4 / 5x5
+// symmetric eigen-solve is a fully unrolled cyclic Jacobi whose indices are all compile-time
+// constants, so the matrices live in VGPRs. The 12x12 solve (M^T M), 90 % of the time when one
+// thread ran it cyclically on an LDS arena (1.5 ms per 64-crop batch), is shared by a 16-lane
+// group in registers with a parallel (round-robin) rotation order (eig12_group), so one
+// hypothesis is one 16-lane group.
 #include <math.h>
 
 #include "krrn_common.h"
@@ -25,7 +27,6 @@
 namespace {
 
 constexpr int kPnpMaxP = 1024;
-constexpr int kArena = 300;  // doubles per 12x12 solve: A 144, U 144, w 12
 
 struct Cam {
   double fu, fv, uc, vc;
@@ -107,75 +108,147 @@ __device__ __forceinline__ void eig_small(double (&A)[N * N], double (&w)[N], do
     for (int k = 0; k < N; ++k) V[i * N + k] = U[k * N + i];
 }
 
-// 12x12 symmetric eigen-solve on an LDS arena (element e at arena[e * S]); returns the four
-// eigenvectors of the SMALLEST eigenvalues, smallest first: v4[r * 12 + k].
-__device__ void eig12_arena(double* ar, int S, double (&v4)[48]) {
-  double* A = ar;
-  double* U = ar + 144 * S;
-  double* w = ar + 288 * S;
-#define AA(i) A[(i) * S]
-#define UU(i) U[(i) * S]
-  for (int i = 0; i < 144; ++i) UU(i) = (i % 13 == 0) ? 1.0 : 0.0;
-  for (int sweep = 0; sweep < 40; ++sweep) {
-    double off = 0.0, tot = 0.0;
-#pragma unroll 12
-    for (int e = 0; e < 144; ++e) {
-      const double a = AA(e);
-      tot += a * a;
-      if (e % 13 != 0) off += a * a;
+// f64 lane shuffle (two ds_bpermute)
+__device__ __forceinline__ double shfl_f64(double v, int src) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __shfl((int)(unsigned)b, src), hi = __shfl((int)(unsigned)(b >> 32), src);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// v[i] for a per-lane i: select chain (a runtime index into a register array would go to scratch)
+template <int N>
+__device__ __forceinline__ double pick(const double (&v)[N], int i) {
+  double r = v[0];
+#pragma unroll
+  for (int j = 1; j < N; ++j) r = (i == j) ? v[j] : r;
+  return r;
+}
+
+// v[i] = x for a per-lane / runtime i (select chain, registers only)
+template <int N>
+__device__ __forceinline__ void put(double (&v)[N], int i, double x) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = (i == j) ? x : v[j];
+}
+
+// 12x12 symmetric eigen-solve (M^T M of EPnP) by the 16 lanes of an aligned lane group, lanes
+// 12..15 idle: lane r < 12 holds row r of A and of U (eigenvectors as columns) in registers.
+// Parallel-ordered Jacobi (round-robin / circle schedule): a sweep is 11 steps, each rotating 6
+// disjoint pairs (p, q) at once -- lane r is in exactly one pair, so every lane computes its pair's
+// rotation (the two lanes of a pair from identical inputs, a[p][q] taken from lane p), then
+// A <- A J (each lane's own row, all 6 pairs' (c, s) shuffled in), A <- J^T A (row r combined with
+// its partner's row), U <- U J. The cyclic one-rotation-at-a-time order had a dependent f64
+// (theta, sqrt, division) chain per rotation, 66 per sweep; here 11 per sweep. oracle/pnp_ref.c
+// (jacobi12_par) restates the same schedule and expressions. Convergence: off(A) <= 1e-30 |A|^2
+// with the row sums reduced over the group by a fixed butterfly (identical in every lane).
+// Rotation arithmetic without FMA contraction (as the gcc-built oracle).
+__device__ __forceinline__ int rr_partner(int k, int r) {  // step k's partner of r (0 <= r < 12)
+  return r == 11 ? k : (r == k ? 11 : (2 * k - r + 11) % 11);
+}
+
+__device__ __forceinline__ double group_sum16(double v) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ void eig12_group(const double (&m)[78], double (&v4)[48]) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63, r = lane & 15, base = lane & ~15;
+  const bool act = r < 12;
+  double a[12], u[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int lo = i < j ? i : j, hi = i < j ? j : i;
+      const int e = lo * 12 - lo * (lo - 1) / 2 + (hi - lo);  // packed upper triangle, row-major
+      v = (r == i) ? m[e] : v;
     }
+    a[j] = v;
+    u[j] = (r == j) ? 1.0 : 0.0;
+  }
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double tot = 0.0, off = 0.0;
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        const double x2 = a[j] * a[j];
+        tot += x2;
+        if (j != r) off += x2;
+      }
+    }
+    tot = group_sum16(tot);
+    off = group_sum16(off);
     if (off <= 1e-30 * tot || off < 1e-300) break;
-    for (int p = 0; p < 12; ++p) {
-      for (int q = p + 1; q < 12; ++q) {
-        const double apq = AA(p * 12 + q);
-        const double app = AA(p * 13), aqq = AA(q * 13);
-        // negligible against both diagonal entries (below their f64 resolution): skip
-        if (fabs(apq) < 1e-300 || fabs(apq) < 1e-18 * sqrt(fabs(app * aqq))) continue;
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+      const int pr = act ? rr_partner(k, r) : r;
+      const int lo = r < pr ? r : pr, hi = r < pr ? pr : r;
+      const double d = pick(a, r);                            // own diagonal
+      const double apq = shfl_f64(pick(a, pr), base + lo);    // a[lo][hi], from lane lo
+      const double dp = shfl_f64(d, base + pr);               // partner's diagonal
+      const double app = r == lo ? d : dp, aqq = r == lo ? dp : d;
+      double c = 1.0, sn = 0.0;
+      if (act && !(fabs(apq) < 1e-300 || fabs(apq) < 1e-18 * sqrt(fabs(app * aqq)))) {
         const double theta = (aqq - app) / (2.0 * apq);
         const double tt = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-        const double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
-        double cp[12], cq[12];
+        c = 1.0 / sqrt(tt * tt + 1.0);
+        sn = tt * c;
+      }
+      // the 6 pairs of step k: (k, 11) and ((k + i) % 11, (k - i) % 11), i = 1..5; (c, s) from the lower lane
+      double cs[6], ss[6];
+      int pp[6], qq[6];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) { cp[k] = AA(k * 12 + p); cq[k] = AA(k * 12 + q); }
+      for (int i = 0; i < 6; ++i) {
+        const int x = i == 0 ? k : (k + i) % 11, y = i == 0 ? 11 : (k - i + 11) % 11;
+        pp[i] = x < y ? x : y;
+        qq[i] = x < y ? y : x;
+        cs[i] = shfl_f64(c, base + pp[i]);
+        ss[i] = shfl_f64(sn, base + pp[i]);
+      }
+      // A <- A J: own row, columns (p_i, q_i)
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-          AA(k * 12 + p) = c * cp[k] - s * cq[k];
-          AA(k * 12 + q) = s * cp[k] + c * cq[k];
-        }
+      for (int i = 0; i < 6; ++i) {
+        const double xp = a[pp[i]], xq = a[qq[i]];
+        a[pp[i]] = cs[i] * xp - ss[i] * xq;
+        a[qq[i]] = ss[i] * xp + cs[i] * xq;
+      }
+      // A <- J^T A: row lo' = c row lo - s row hi, row hi' = s row lo + c row hi
 #pragma unroll
-        for (int k = 0; k < 12; ++k) { cp[k] = AA(p * 12 + k); cq[k] = AA(q * 12 + k); }
+      for (int j = 0; j < 12; ++j) {
+        const double y = shfl_f64(a[j], base + pr);
+        a[j] = r == lo ? c * a[j] - sn * y : sn * y + c * a[j];
+      }
+      // U <- U J
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-          AA(p * 12 + k) = c * cp[k] - s * cq[k];
-          AA(q * 12 + k) = s * cp[k] + c * cq[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 12; ++k) { cp[k] = UU(k * 12 + p); cq[k] = UU(k * 12 + q); }
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-          UU(k * 12 + p) = c * cp[k] - s * cq[k];
-          UU(k * 12 + q) = s * cp[k] + c * cq[k];
-        }
+      for (int i = 0; i < 6; ++i) {
+        const double xp = u[pp[i]], xq = u[qq[i]];
+        u[pp[i]] = cs[i] * xp - ss[i] * xq;
+        u[qq[i]] = ss[i] * xp + cs[i] * xq;
       }
     }
   }
-  for (int i = 0; i < 12; ++i) w[i * S] = AA(i * 13);
+  double w[12];
+  const double wd = pick(a, r);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) w[i] = shfl_f64(wd, base + i);
   // the 4 smallest eigenvalues in ascending order (ties: lower column first)
   unsigned used = 0;
-  for (int r = 0; r < 4; ++r) {
-    int m = -1;
+  for (int q4 = 0; q4 < 4; ++q4) {
+    int mi = -1;
     double wm = 0.0;
+#pragma unroll
     for (int j = 0; j < 12; ++j) {
       if (used & (1u << j)) continue;
-      const double wj = w[j * S];
-      if (m < 0 || wj < wm) { m = j; wm = wj; }
+      if (mi < 0 || w[j] < wm) { mi = j; wm = w[j]; }
     }
-    used |= 1u << m;
+    used |= 1u << mi;
+    const double um = pick(u, mi);
 #pragma unroll
-    for (int k = 0; k < 12; ++k) v4[r * 12 + k] = UU(k * 12 + m);
+    for (int kk = 0; kk < 12; ++kk) v4[q4 * 12 + kk] = shfl_f64(um, base + kk);
   }
-#undef AA
-#undef UU
 }
 
 // least squares min ||A x - b|| (A is 6 x N) through the pseudo-inverse from eig(A^T A)
@@ -296,35 +369,13 @@ struct Pts {
   }
 };
 
-// Point-loop sums and the 12x12 solve of EPnP, evaluated either by one thread (a RANSAC
-// hypothesis, SerialSum) or by one wave with the points spread over the 64 lanes and a
-// butterfly reduction (the refinement on all inliers, WaveSum). The small dense algebra
-// between the sums is replicated in every lane, which costs one wave's time.
-struct SerialSum {
-  double* arena;  // this thread's arena (stride S)
-  int S;
-  template <int NV, class F>
-  __device__ __forceinline__ void operator()(int n, F f, double (&acc)[NV]) const {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-    for (int i = 0; i < n; ++i) f(i, acc);
-  }
-  __device__ __forceinline__ void eig12(const double (&m)[78], double (&v4)[48]) const {
-    int e = 0;
-#pragma unroll
-    for (int i = 0; i < 12; ++i)
-#pragma unroll
-      for (int j = i; j < 12; ++j, ++e) {
-        arena[(i * 12 + j) * S] = m[e];
-        arena[(j * 12 + i) * S] = m[e];
-      }
-    eig12_arena(arena, S, v4);
-  }
-};
-
+// Point-loop sums and the 12x12 solve of EPnP, evaluated either per 16-lane group (a RANSAC
+// hypothesis: GroupSum, the point sums replicated in every lane) or by one wave with the points
+// spread over the 64 lanes and a butterfly reduction (the refinement on all inliers, WaveSum).
+// The small dense algebra between the sums is replicated in every lane; the 12x12 solve is
+// eig12_group in each 16-lane group (WaveSum: all 4 groups solve the same replicated matrix).
 struct WaveSum {
   int lane;
-  double* arena;  // one shared arena (stride 1), solved by lane 0
   template <int NV, class F>
   __device__ __forceinline__ void operator()(int n, F f, double (&acc)[NV]) const {
 #pragma unroll
@@ -338,23 +389,19 @@ struct WaveSum {
       acc[k] = v;
     }
   }
-  __device__ __forceinline__ void eig12(const double (&m)[78], double (&v4)[48]) const {
-    __syncthreads();
-    if (lane == 0) {
-      int e = 0;
-      for (int i = 0; i < 12; ++i)
-        for (int j = i; j < 12; ++j, ++e) {
-          arena[i * 12 + j] = m[e];
-          arena[j * 12 + i] = m[e];
-        }
-      double r[48];
-      eig12_arena(arena, 1, r);
-      for (int k = 0; k < 48; ++k) arena[k] = r[k];
-    }
-    __syncthreads();
+  __device__ __forceinline__ void eig12(const double (&m)[78], double (&v4)[48]) const { eig12_group(m, v4); }
+};
+
+// One RANSAC hypothesis per aligned 16-lane group: the point sums (5 points) replicated in every
+// lane, the 12x12 solve spread over the group (eig12_group).
+struct GroupSum {
+  template <int NV, class F>
+  __device__ __forceinline__ void operator()(int n, F f, double (&acc)[NV]) const {
 #pragma unroll
-    for (int k = 0; k < 48; ++k) v4[k] = arena[k];
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    for (int i = 0; i < n; ++i) f(i, acc);
   }
+  __device__ __forceinline__ void eig12(const double (&m)[78], double (&v4)[48]) const { eig12_group(m, v4); }
 };
 
 __device__ __forceinline__ void alphas_of(const double* p, const double cws[4][3], const double* ci, double a[4]) {
@@ -684,79 +731,95 @@ __device__ void load_corr(int b, const float* xyz, int HW, const long long* choo
   }
 }
 
-#ifndef KRRN_PNP_HPB
-#define KRRN_PNP_HPB 50  // measured (ms/step): 16 -> 15.98, 25 -> 15.90, 32 -> 15.83, 50 -> 15.64-15.77, 64 -> 15.75
-#endif
-constexpr int kHypPerBlock = KRRN_PNP_HPB;
-
-// Phase 1: one thread per RANSAC hypothesis; grid (B, ceil(H / kHypPerBlock)). The blocks are
-// long-lived (~1 ms of serial f64 solves) and run beside the fusion / TBase launches: 50
-// hypotheses per block (H = 100 -> 2 blocks per crop, 125 KB of LDS each, one per CU) confines
-// the kernel to ~128 CUs and leaves the rest of the chip whole, which beats spreading 448
-// quarter-wave blocks of 16 over every CU (15.7 vs 16.0 ms per step). Writes the f32 pose (R, t: the precision the inlier
-// test uses) and the inlier count of every hypothesis.
-__global__ __launch_bounds__(kHypPerBlock) void pnp_hyp_kernel(
+// Phase 1: one RANSAC hypothesis per 16-lane group, 16 per block, grid (B, ceil(H / 16)). The
+// group replicates the hypothesis' 5-point EPnP over its lanes except the 12x12 solve, which it
+// shares (eig12_group), and splits the P inlier tests over its 16 lanes. Writes the f32 pose (R,
+// t: the precision the inlier test uses) and the inlier count of every hypothesis. LDS: the P
+// correspondences only (5 KB at P = 256), so the blocks co-reside with the fusion / TBase
+// launches they run beside.
+constexpr int kHypPerBlock = 16;
+__global__ __launch_bounds__(256) void pnp_hyp_kernel(
     const float* __restrict__ xyz, int HW, const long long* __restrict__ choose, int N, const int* __restrict__ sel,
     int P, const float* __restrict__ xmap, const float* __restrict__ ymap, const float* __restrict__ K4,
     const double* __restrict__ extent, const double* __restrict__ lfb, const int* __restrict__ subsets, int H,
     float thr, float* __restrict__ hyp_pose, int* __restrict__ hyp_cnt) {
-  // LDS sized by P (dynamic): the arena, then P object + P image points. At P = 256 this is
-  // 43.5 KB instead of 58.9 KB for kPnpMaxP: the kernel's blocks live ~1 ms beside the fusion /
-  // TBase launches, whose co-residency on those CUs the LDS footprint decides (16.42 -> 16.26
-  // ms/step measured)
-  extern __shared__ double pnp_dyn[];
-  double* sarena = pnp_dyn;
-  float* sobj = reinterpret_cast<float*>(pnp_dyn + kArena * kHypPerBlock);
+  extern __shared__ float pnp_corr[];
+  float* sobj = pnp_corr;
   float* simg = sobj + 3 * P;
   const int b = blockIdx.x;
   const Cam cam = {K4[4 * b + 0], K4[4 * b + 1], K4[4 * b + 2], K4[4 * b + 3]};
   load_corr(b, xyz, HW, choose, N, sel, P, xmap, ymap, extent, lfb, sobj, simg);
   __syncthreads();
-  const int h = blockIdx.y * kHypPerBlock + threadIdx.x;
-  if (h >= H) return;
+  const int r = threadIdx.x & 15;
+  const int h = blockIdx.y * kHypPerBlock + (threadIdx.x >> 4);
+  const int hs = h < H ? h : H - 1;  // a tail group solves a duplicate (whole groups stay active) and writes nothing
   int ids[5];
-  for (int i = 0; i < 5; ++i) ids[i] = subsets[((long long)b * H + h) * 5 + i];
+  for (int i = 0; i < 5; ++i) ids[i] = subsets[((long long)b * H + hs) * 5 + i];
   Pts sub{sobj, simg, ids, 5};
   double R[9], t[3];
-  epnp(SerialSum{sarena + threadIdx.x, kHypPerBlock}, sub, cam, R, t);
+  epnp(GroupSum{}, sub, cam, R, t);
   float Rf[9], tf[3];
   for (int i = 0; i < 9; ++i) Rf[i] = (float)R[i];
   for (int i = 0; i < 3; ++i) tf[i] = (float)t[i];
   const float thr2 = thr * thr;
   int cnt = 0;
-  for (int p = 0; p < P; ++p) cnt += is_inlier(Rf, tf, sobj + 3 * p, simg + 2 * p, cam, thr2) ? 1 : 0;
+  for (int p = r; p < P; p += 16) cnt += is_inlier(Rf, tf, sobj + 3 * p, simg + 2 * p, cam, thr2) ? 1 : 0;
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if (h >= H || r != 0) return;
   float* o = hyp_pose + ((long long)b * H + h) * 12;
   for (int i = 0; i < 9; ++i) o[i] = Rf[i];
   for (int i = 0; i < 3; ++i) o[9 + i] = tf[i];
   hyp_cnt[(long long)b * H + h] = cnt;
 }
 
-// Phase 2: one wave per crop. Best hypothesis (most inliers, lowest index; accepted with >= 5
-// inliers), its ordered inlier set, then EPnP on all inliers with the point sums spread over
-// the 64 lanes.
+// cv::RANSACUpdateNumIters (ptsetreg.cpp): iterations needed for `conf` given outlier ratio ep
+__device__ __forceinline__ int ransac_update_niters(double conf, double ep, int model_points, int max_iters) {
+  conf = fmin(fmax(conf, 0.0), 1.0);
+  ep = fmin(fmax(ep, 0.0), 1.0);
+  double num = fmax(1.0 - conf, 2.2250738585072014e-308);
+  double denom = 1.0 - pow(1.0 - ep, (double)model_points);
+  if (denom < 2.2250738585072014e-308) return 0;
+  num = log(num);
+  denom = log(denom);
+  return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
+}
+
+// Phase 2: one wave per crop. The RANSAC loop of ptsetreg.cpp over the scored hypotheses in
+// order: hypothesis h is considered while h < niters; a strictly better count (and >= 5 inliers:
+// goodCount > max(maxGoodCount, modelPoints - 1)) becomes the best and lowers niters to
+// RANSACUpdateNumIters(confidence, outlier ratio, 5, niters). Then the best hypothesis' ordered
+// inlier set and EPnP on all inliers with the point sums spread over the 64 lanes.
 __global__ __launch_bounds__(64) void pnp_refine_kernel(
     const float* __restrict__ xyz, int HW, const long long* __restrict__ choose, int N, const int* __restrict__ sel,
     int P, const float* __restrict__ xmap, const float* __restrict__ ymap, const float* __restrict__ K4,
-    const double* __restrict__ extent, const double* __restrict__ lfb, int H, float thr,
+    const double* __restrict__ extent, const double* __restrict__ lfb, int H, float thr, float conf,
     const float* __restrict__ hyp_pose, const int* __restrict__ hyp_cnt, float* __restrict__ Rout,
     float* __restrict__ tout, int* __restrict__ inl_out, unsigned char* __restrict__ mask_out) {
   __shared__ float sobj[kPnpMaxP * 3];
   __shared__ float simg[kPnpMaxP * 2];
   __shared__ int slist[kPnpMaxP];
-  __shared__ double sarena[kArena];
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const Cam cam = {K4[4 * b + 0], K4[4 * b + 1], K4[4 * b + 2], K4[4 * b + 3]};
   load_corr(b, xyz, HW, choose, N, sel, P, xmap, ymap, extent, lfb, sobj, simg);
   __syncthreads();
-  int key = -1;
-  for (int h = lane; h < H; h += 64) key = max(key, hyp_cnt[(long long)b * H + h] * 4096 + (4095 - h));
-  for (int off = 32; off > 0; off >>= 1) key = max(key, __shfl_xor(key, off));
-  const int best_cnt = key >= 0 ? key / 4096 : 0;
-  const int best_h = key >= 0 ? 4095 - (key % 4096) : -1;
-  const bool ok = best_h >= 0 && best_cnt >= 5;
+  // the sequential scan (every lane, identical): counts come 64 at a time through one load each
+  int best_h = -1, best_cnt = 0, niters = H;
+  for (int h0 = 0; h0 < niters; h0 += 64) {
+    const int mine = h0 + lane < H ? hyp_cnt[(long long)b * H + h0 + lane] : 0;
+    for (int i = 0; i < 64 && h0 + i < niters; ++i) {
+      const int cnt = __shfl(mine, i);
+      if (cnt > (best_cnt > 4 ? best_cnt : 4)) {
+        best_cnt = cnt;
+        best_h = h0 + i;
+        niters = ransac_update_niters((double)conf, (double)(P - cnt) / P, 5, niters);
+      }
+    }
+  }
+  const bool ok = best_h >= 0;
   float Rf[9], tf[3];
-  if (best_h >= 0) {
+  if (ok) {
     const float* hp = hyp_pose + ((long long)b * H + best_h) * 12;
     for (int i = 0; i < 9; ++i) Rf[i] = hp[i];
     for (int i = 0; i < 3; ++i) tf[i] = hp[9 + i];
@@ -777,7 +840,7 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
   if (ok && n >= 5) {
     Pts inl{sobj, simg, slist, n};
     double R[9], t[3];
-    epnp(WaveSum{lane, sarena}, inl, cam, R, t);
+    epnp(WaveSum{lane}, inl, cam, R, t);
     if (lane == 0) {
       for (int i = 0; i < 9; ++i) Rout[9 * b + i] = (float)R[i];
       for (int i = 0; i < 3; ++i) tout[3 * b + i] = (float)t[i];
@@ -795,19 +858,20 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
 
 KRRN_API int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choose, int N, const int* sel, int P,
                                  const float* xmap, const float* ymap, const float* K4, const double* extent,
-                                 const double* lfborder, const int* subsets, int H, float thr, float* workspace,
-                                 float* R, float* t, int* inliers, unsigned char* inlier_mask, int B, void* stream) {
+                                 const double* lfborder, const int* subsets, int H, float thr, float conf,
+                                 float* workspace, float* R, float* t, int* inliers, unsigned char* inlier_mask, int B,
+                                 void* stream) {
   if (!xyz || !choose || !sel || !xmap || !ymap || !K4 || !extent || !lfborder || !subsets || !workspace || !R ||
       !t || !inliers)
     return KRRN_EARG;
-  if (B < 1 || P < 5 || P > kPnpMaxP || H < 1 || H > 4095 || N < 1 || HW < 1) return KRRN_ESHAPE;
+  if (B < 1 || P < 5 || P > kPnpMaxP || H < 1 || H > 4095 || N < 1 || HW < 1 || !(conf >= 0.f && conf <= 1.f))
+    return KRRN_ESHAPE;
   hipStream_t s = (hipStream_t)stream;
   float* hyp_pose = workspace;
   int* hyp_cnt = reinterpret_cast<int*>(workspace + (size_t)B * H * 12);
-  const size_t hyp_lds = sizeof(double) * kArena * kHypPerBlock + sizeof(float) * 5 * (size_t)P;
-  hipLaunchKernelGGL(pnp_hyp_kernel, dim3(B, krrn_cdiv(H, kHypPerBlock)), dim3(kHypPerBlock), hyp_lds, s, xyz, HW, choose,
-                     N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
+  hipLaunchKernelGGL(pnp_hyp_kernel, dim3(B, krrn_cdiv(H, kHypPerBlock)), dim3(256), sizeof(float) * 5 * (size_t)P, s,
+                     xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
   hipLaunchKernelGGL(pnp_refine_kernel, dim3(B), dim3(64), 0, s, xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent,
-                     lfborder, H, thr, hyp_pose, hyp_cnt, R, t, inliers, inlier_mask);
+                     lfborder, H, thr, conf, hyp_pose, hyp_cnt, R, t, inliers, inlier_mask);
   return krrn_launch_status();
 }

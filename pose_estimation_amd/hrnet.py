@@ -29,11 +29,10 @@ import torch.nn as nn
 from . import ops
 from .config import load_hrnet_spec
 from .ops import Act, pad4
-from .runtime import add_conv_group, Plan, add_conv, ptr
+from .runtime import add_conv_group, add_small_group, Plan, add_conv, ptr
 
-# HRNet branch convs as per-branch chains on plan streams (default: measured 23.5 ms/step) or
-# as grouped launches, one per block depth (KRRN_HR_GROUP=1: 25.4 ms/step; the grouped launch
-# is bound by its slowest member and loses the cross-branch overlap of the streams)
+# HRNet branch convs as per-branch chains on plan streams (KRRN_HR_GROUP=0) or as grouped
+# launches, one per block depth (KRRN_HR_GROUP=1)
 HR_GROUP = os.environ.get("KRRN_HR_GROUP", "0") == "1"
 # deconv_layer folded through the linear last_layer_2 (build_hrnet_plan)
 DECONV_FOLD = os.environ.get("KRRN_DECONV_FOLD", "1") == "1"
@@ -230,18 +229,28 @@ class _Builder:
             self.emit_conv(x, spec, out, res, relu)
         return out
 
-    def emit_small(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
+    @staticmethod
+    def small_problem(x: Act, spec, out: Act, res: Optional[Act], relu: bool) -> dict:
+        """krrn_conv3x3_small_f32's arguments (SmallDesc fields) plus the breakdown's FLOP counts."""
         np_ = pad4(spec.cout)
         M = x.B * out.H * out.W
         ntiles = (np_ + 15) // 16
         nw, ks = ops.small_conv_config(M, ntiles, spec.cin_p)
-        self.plan.add("krrn_conv3x3_small_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(spec.wt[0]), np_,
-                      np_, ptr(spec.scale), ptr(spec.bias), ptr(res.t) if res is not None else ptr(None),
-                      res.cs if res is not None else 0, res.co if res is not None else 0, ptr(out.t), out.cs, out.co,
-                      int(relu), nw, ks,
-                      meta=dict(kernel=f"conv3x3_small<{nw},{ks}>", flops=2.0 * spec.cin * spec.cout * 9 * M, tag=tag,
-                                M=M, N=np_, K=spec.cin_p * 9, splits=1,
-                                mfma_flops=2.0 * 16 * ((9 * spec.cin_p // 4 + 3) // 4) * 16 * ntiles * M))
+        return dict(x=ptr(x.t), in_cs=x.cs, in_co=x.co, B=x.B, H=x.H, W=x.W, cin=spec.cin_p, wt=ptr(spec.wt[0]),
+                    N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
+                    res=ptr(res.t) if res is not None else ptr(None), res_cs=res.cs if res is not None else 0,
+                    res_co=res.co if res is not None else 0, out=ptr(out.t), out_cs=out.cs, out_co=out.co,
+                    relu=int(relu), nw=nw, ks=ks, flops=2.0 * spec.cin * spec.cout * 9 * M,
+                    mfma_flops=2.0 * 16 * ((9 * spec.cin_p // 4 + 3) // 4) * 16 * ntiles * M)
+
+    def emit_small(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
+        p = self.small_problem(x, spec, out, res, relu)
+        M = x.B * out.H * out.W
+        self.plan.add("krrn_conv3x3_small_f32", p["x"], p["in_cs"], p["in_co"], p["B"], p["H"], p["W"], p["cin"], p["wt"],
+                      p["N"], p["n_store"], p["scale"], p["bias"], p["res"], p["res_cs"], p["res_co"], p["out"],
+                      p["out_cs"], p["out_co"], p["relu"], p["nw"], p["ks"],
+                      meta=dict(kernel=f"conv3x3_small<{p['nw']},{p['ks']}>", flops=p["flops"], tag=tag, M=M, N=p["N"],
+                                K=spec.cin_p * 9, splits=1, mfma_flops=p["mfma_flops"]))
 
     def emit_wino(self, x: Act, spec, U: torch.Tensor, out: Act, res: Optional[Act], relu: bool,
                   tag: str = "conv"):
@@ -280,34 +289,38 @@ class _Builder:
                      out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=osy, osx=osx, ooy=ooy,
                      oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag)
 
-    def conv_problem(self, x: Act, conv: nn.Module, bn: Optional[nn.Module], res: Optional[Act] = None,
-                     relu: bool = False) -> Tuple[dict, Act]:
-        """A stride-1 / stride-2 conv as one problem of a grouped launch (no emission)."""
-        spec = ops.make_conv(conv, bn, self.dev, cin_p=x.cp)
-        self.specs.append(spec)
-        Ho, Wo = ops.conv_out_hw(spec, x.H, x.W)
-        out = self.act(Ho, Wo, spec.cout)
-        np_ = pad4(spec.cout)
-        pr = dict(x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=Ho, Wg=Wo,
-                  in_s=spec.stride, taps=spec.taps[0], wt=ptr(spec.wt[0]), N=np_, n_store=np_,
-                  scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(res.t) if res is not None else None,
-                  res_cs=res.cs if res is not None else 0, res_co=res.co if res is not None else 0,
-                  out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=Ho, Wo=Wo, relu=relu, cin=spec.cin,
-                  cout=spec.cout)
-        return pr, out
+    def small_grouped(self, xs: List[Act], convs: List[Tuple[nn.Module, nn.Module]], res: Optional[List[Act]],
+                      tag: str) -> Optional[List[Act]]:
+        """The i-th conv on xs[i] for every branch as ONE krrn_conv3x3_small_group_f32 launch, or
+        None (nothing emitted) when one of them is not a small-conv problem."""
+        specs = []
+        for x, (conv, bn) in zip(xs, convs):
+            spec = ops.make_conv(conv, bn, self.dev, cin_p=x.cp)
+            if not ops.small_conv_eligible(spec, x):
+                return None
+            specs.append(spec)
+        self.specs.extend(specs)
+        outs = [self.act(x.H, x.W, spec.cout) for x, spec in zip(xs, specs)]
+        probs = [self.small_problem(x, spec, o, res[i] if res is not None else None, True)
+                 for i, (x, spec, o) in enumerate(zip(xs, specs, outs))]
+        add_small_group(self.plan, probs, tag=tag)
+        return outs
 
-    def branches_grouped(self, xs: List[Act], m: "HighResolutionModule") -> List[Act]:
+    def branches_grouped(self, xs: List[Act], m: "HighResolutionModule") -> Optional[List[Act]]:
         """All branches of a module, block by block: the j-th conv of every branch in ONE grouped
-        launch (myhrnet.py:226-231 runs branch i's BasicBlocks on x[i]; nothing couples them)."""
+        small-conv launch (myhrnet.py:226-231 runs branch i's BasicBlocks on x[i]; nothing couples
+        them). None (nothing emitted) when a branch conv is not a small-conv problem: every depth
+        has the first one's shapes, so that is decided before anything is emitted."""
         cur = list(xs)
         for bi in range(len(m.branches[0])):
             blks = [m.branches[i][bi] for i in range(m.num_branches)]
-            probs, hs = zip(*[self.conv_problem(cur[i], b.conv1, b.bn1, relu=True) for i, b in enumerate(blks)])
-            add_conv_group(self.plan, list(probs), tag="hr_branch_conv1")
-            probs, ys = zip(*[self.conv_problem(hs[i], b.conv2, b.bn2, res=cur[i], relu=True)
-                              for i, b in enumerate(blks)])
-            add_conv_group(self.plan, list(probs), tag="hr_branch_conv2")
-            cur = list(ys)
+            hs = self.small_grouped(cur, [(b.conv1, b.bn1) for b in blks], None, "hr_branch_conv1")
+            if hs is None:
+                assert bi == 0
+                return None
+            ys = self.small_grouped(hs, [(b.conv2, b.bn2) for b in blks], cur, "hr_branch_conv2")
+            assert ys is not None  # conv2 has conv1's output shape and width
+            cur = ys
         return cur
 
     def resize(self, x: Act, out: Act, add: Optional[Act] = None, align: bool = False, relu: bool = False):
@@ -339,11 +352,11 @@ class _Builder:
         plan = self.plan
         nb = m.num_branches
         side = list(range(1, nb))
-        groupable = HR_GROUP and 1 < nb <= 4 and all(len(m.branches[i]) == len(m.branches[0]) for i in range(nb)) and all(
+        groupable = HR_GROUP and SMALL_CONV and 1 < nb <= 4 and all(
+            len(m.branches[i]) == len(m.branches[0]) for i in range(nb)) and all(
             isinstance(b, BasicBlock) and b.downsample is None for br in m.branches for b in br)
-        if groupable:
-            ys = self.branches_grouped(xs, m)
-        else:
+        ys = self.branches_grouped(xs, m) if groupable else None
+        if ys is None:
             ys = []
             plan.fork(side)
             for i, x in enumerate(xs):

@@ -8,8 +8,9 @@ generator, :406-408), object points = xyz * extent + lfborder (f64, :415-421), i
 = full-frame (x, y) of the same pixels, EPnP hypotheses, 1 px reprojection threshold,
 EPnP refinement on the inliers, R as a matrix (the rvec -> kornia Rodrigues step is an
 identity on R). The reference asserts B == 1 (:402); any B works here, one workgroup per crop.
-RANSAC subsets: H = 100 hypotheses per crop (cv2's default iterationsCount), drawn on the
-device (krrn_ransac_subsets) unless given explicitly.
+RANSAC: H = 100 hypotheses per crop (cv2's default iterationsCount), drawn on the device
+(krrn_ransac_subsets) unless given explicitly, scored in parallel and selected by cv2's own loop
+(in order, stopping at its adaptive iteration count for confidence 0.9999, :426).
 """
 from __future__ import annotations
 
@@ -23,6 +24,7 @@ from . import _lib
 NUM_POINTS = 256
 N_HYP = 100
 THRESHOLD = 1.0
+CONFIDENCE = 0.9999
 
 _seeds: Dict[int, torch.Tensor] = {}
 
@@ -79,7 +81,7 @@ def get_pose(pred, data, num_points: int = NUM_POINTS, n_hyp: int = N_HYP, thr: 
     mask = torch.empty((B, P_), dtype=torch.uint8, device=dev)
     ws = torch.empty((B * n_hyp * 13,), dtype=torch.float32, device=dev)
     _lib.check(lib.krrn_pnp_ransac_f32(ptr(xyz), H * W, ptr(choose), N, ptr(sel), P_, ptr(xm), ptr(ym), ptr(K4),
-                                       ptr(ext), ptr(lfb), ptr(subsets), n_hyp, float(thr), ptr(ws), ptr(R), ptr(t),
+                                       ptr(ext), ptr(lfb), ptr(subsets), n_hyp, float(thr), CONFIDENCE, ptr(ws), ptr(R), ptr(t),
                                        ptr(inl), ptr(mask), B, stream), "krrn_pnp_ransac_f32")
     if return_info:
         return R, t, {"inliers": inl, "mask": mask, "sel": sel, "subsets": subsets, "workspace": ws}
@@ -103,5 +105,5 @@ def add_pose_ops(plan: Plan, xyz: torch.Tensor, choose: torch.Tensor, B: int, N:
     plan.add("krrn_randperm_i32", ptr(seed), 5, N, P_, B, ptr(sel))
     plan.add("krrn_ransac_subsets", ptr(seed), 6, B, n_hyp, P_, ptr(subsets))
     plan.add("krrn_pnp_ransac_f32", ptr(xyz), H * W, ptr(choose), N, ptr(sel), P_, ptr(xm), ptr(ym), ptr(K4), ptr(ext),
-             ptr(lfb), ptr(subsets), n_hyp, float(thr), ptr(ws), ptr(R), ptr(t), ptr(inl), ptr(mask), B)
+             ptr(lfb), ptr(subsets), n_hyp, float(thr), CONFIDENCE, ptr(ws), ptr(R), ptr(t), ptr(inl), ptr(mask), B)
     return R, t, inl, dict(sel=sel, subsets=subsets, mask=mask)

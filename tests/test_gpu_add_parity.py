@@ -21,7 +21,7 @@ from oracle import pnp as opnp
 from pose_estimation_amd import pose
 from pose_estimation_amd.metric import Metric
 
-from test_gpu_pnp import K4, _scene
+from test_gpu_pnp import K4, _cv2_select, _scene
 
 pytestmark = pytest.mark.gpu
 
@@ -48,7 +48,7 @@ def test_add_auc_matches_oracle(dev, noise_px):
             pix = data["choose"][b, 0, s]
             obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
             img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
-            best_h = int(np.argmax(hcnt[b]))
+            best_h = _cv2_select(hcnt[b], len(s))
             Ro, to, _, _, _ = opnp.pnp_ransac(obj, img, K4, subs[b, best_h:best_h + 1].numpy(), 1.0)
             target = torch.from_numpy(model @ Rgt[b].T + tgt[b]).float().to(dev)
             pg = torch.from_numpy(model @ R[b].cpu().double().numpy().T + t[b].cpu().double().numpy()).float().to(dev)

@@ -256,3 +256,40 @@ def test_conv3x3_small(dev, B, cin, cout, H, W, co, nw, ks):
     got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
     torch.testing.assert_close(got, ref, **TOL)
     assert torch.count_nonzero(out.t[..., np_:]).item() == 0
+
+
+def test_conv3x3_small_group(dev):
+    """krrn_conv3x3_small_group_f32: the four W18 branch shapes (and their (nw, ks) configs) in one
+    launch give exactly the single launches' outputs."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, SmallDesc, ptr
+    import ctypes
+    L = _lib.lib()
+    st = P(torch.cuda.current_stream().cuda_stream)
+    B = 6
+    g = torch.Generator().manual_seed(7)
+    descs, singles = [], []
+    for cin, H, nw, ks in [(18, 30, 2, 1), (36, 15, 3, 2), (72, 8, 3, 4), (144, 4, 3, 4)]:
+        cp = ops.pad4(cin)
+        conv = nn.Conv2d(cin, cin, 3, 1, 1, bias=False)
+        with torch.no_grad():
+            conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
+        spec = ops.make_conv(conv, _bn(cin, g), dev, cin_p=cp)
+        xa = _nhwc(torch.randn(B, cin, H, H, generator=g), dev)
+        ra = _nhwc(torch.randn(B, cin, H, H, generator=g), dev)
+        outs = [torch.full((B, H, H, cp), float("nan"), device=dev) for _ in range(2)]
+        args = dict(in_=ptr(xa.t), in_cs=xa.cs, in_co=0, B=B, H=H, W=H, cin=cp, wt=ptr(spec.wt[0]), N=cp, n_store=cp,
+                    scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(ra.t), res_cs=ra.cs, res_co=0, out_cs=cp,
+                    out_co=0, relu=1, nw=nw, ks=ks)
+        descs.append(SmallDesc(out=ptr(outs[0]), **args))
+        a = dict(args, out=ptr(outs[1]))
+        _lib.check(L.krrn_conv3x3_small_f32(a["in_"], a["in_cs"], 0, B, H, H, cp, a["wt"], cp, cp, a["scale"],
+                                            a["bias"], a["res"], a["res_cs"], 0, a["out"], cp, 0, 1, nw, ks, st),
+                   "small conv")
+        singles.append((outs, spec, xa, ra))
+    arr = (SmallDesc * len(descs))(*descs)
+    _lib.check(L.krrn_conv3x3_small_group_f32(ctypes.cast(arr, P), len(descs), st), "small group")
+    torch.cuda.synchronize()
+    for outs, *_ in singles:
+        assert not torch.isnan(outs[0]).any()
+        assert torch.equal(outs[0], outs[1])

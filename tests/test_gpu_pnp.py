@@ -48,6 +48,29 @@ def _scene(B, N, S, seed, outlier_frac=0.1, noise_px=0.0):
     return torch.from_numpy(xyz), data, np.stack(Rs), np.stack(ts)
 
 
+def _update_niters(conf, ep, model_points, max_iters):
+    """cv::RANSACUpdateNumIters (ptsetreg.cpp)."""
+    conf, ep = min(max(conf, 0.0), 1.0), min(max(ep, 0.0), 1.0)
+    num = max(1.0 - conf, np.finfo(np.float64).tiny)
+    denom = 1.0 - (1.0 - ep) ** model_points
+    if denom < np.finfo(np.float64).tiny:
+        return 0
+    num, denom = np.log(num), np.log(denom)
+    return max_iters if (denom >= 0 or -num >= max_iters * (-denom)) else int(np.rint(num / denom))
+
+
+def _cv2_select(cnts, P, conf=np.float32(0.9999)):
+    """ptsetreg.cpp's RANSAC loop over already-scored hypotheses: the selected index."""
+    best, best_cnt, niters, h = -1, 0, len(cnts), 0
+    while h < niters:
+        c = int(cnts[h])
+        if c > max(best_cnt, 4):
+            best, best_cnt = h, c
+            niters = _update_niters(float(conf), (P - c) / P, 5, niters)
+        h += 1
+    return best
+
+
 def test_known_pose_recovery(dev):
     B, N, S = 8, 1000, 120
     xyz, data, Rgt, tgt = _scene(B, N, S, 0)
@@ -89,9 +112,10 @@ def test_matches_oracle_same_subsets(dev, noise_px, cnt_tol, pose_tol):
         pix = data["choose"][b, 0, s]
         obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
         img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
-        best_h = int(np.argmax(hcnt[b]))  # most inliers, lowest index
+        best_h = _cv2_select(hcnt[b], len(s))  # cv2's loop with its adaptive iteration count
         Ro, to, cnt, mask, _ = opnp.pnp_ransac(obj, img, K4, subs[b, best_h:best_h + 1].numpy(), 1.0)
         gcnt = int(info["inliers"][b])
+        assert gcnt == int(hcnt[b][best_h]), (b, gcnt, hcnt[b][best_h])
         assert abs(gcnt - cnt) <= cnt_tol, (b, gcnt, cnt)
         assert np.abs(R[b].cpu().numpy() - Ro).max() < pose_tol
         assert np.abs(t[b].cpu().numpy() - to).max() < pose_tol
@@ -132,3 +156,4 @@ def test_device_rng(dev):
     s = subs.cpu().reshape(-1, 5)
     assert all(len(set(row.tolist())) == 5 for row in s)
     assert s.min() >= 0 and s.max() < 256
+
