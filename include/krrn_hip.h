@@ -117,18 +117,21 @@ int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, i
  * 0 = the register-staged V image. All three give bit-identical results. */
 int krrn_wino_variant(int v);
 
-/* Direct 3x3 / stride 1 / pad 1 conv for narrow layers (the HRNet branches' BasicBlock convs,
- * lib/network/hrnet/myhrnet.py:34-63): NHWC in (in_cs / in_co, cin physical channels, multiple of
- * 4), weights wt [N][9 * cin] (k = tap * cin + c, tap = ky * 3 + kx), out = act(scale[n] * conv +
- * bias[n] (+ res)) for n < n_store. A block stages the input rows of its 64 / ks output pixels
- * (all channels) in LDS once; 16x16x4 f32 MFMAs; nw = 16-channel output tiles per wave (1..3),
- * ks = waves splitting the reduction of one tile (1, 2, 4; partials summed in LDS in order). */
-int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* wt,
-                           int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
-                           int res_co, float* out, int out_cs, int out_co, int relu, int nw, int ks, void* stream);
-/* The arguments of krrn_conv3x3_small_f32 as a struct, and up to 4 independent such convs in ONE
- * launch (the j-th BasicBlock conv of every HRNet branch, myhrnet.py:177-231: the branches are
- * independent until the fuse layer). Each problem computes exactly what krrn_conv3x3_small_f32
+/* Direct conv for narrow layers: 3x3 / pad 1 / stride 1 or 2, or 1x1 / stride 1 (the HRNet
+ * branches' BasicBlock convs, lib/network/hrnet/myhrnet.py:34-63, and the fuse layers' stride-2
+ * downsamples / 1x1 projections, :177-225). NHWC in (in_cs / in_co, H x W input, cin physical
+ * channels, multiple of 4), weights wt [N][ksize^2 * cin] (k = tap * cin + c, tap = ky * ksize + kx),
+ * out (Ho x Wo = the conv's output size) = act(scale[n] * conv + bias[n] (+ res)) for n < n_store.
+ * A block stages the input rows of its 64 / ks output pixels (all channels) in LDS once;
+ * 16x16x4 f32 MFMAs; nw = 16-channel output tiles per wave (1..3), ks = waves splitting the
+ * reduction of one tile (1, 2, 4; partials summed in LDS in order). */
+int krrn_conv_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* wt, int N,
+                        int n_store, const float* scale, const float* bias, const float* res, int res_cs, int res_co,
+                        float* out, int out_cs, int out_co, int relu, int ksize, int stride, int nw, int ks,
+                        void* stream);
+/* The arguments of krrn_conv_small_f32 as a struct, and up to 4 independent such convs in ONE
+ * launch (e.g. the j-th BasicBlock conv of every HRNet branch, myhrnet.py:177-231: the branches
+ * are independent until the fuse layer). Each problem computes exactly what krrn_conv_small_f32
  * computes with the same arguments (bit-identical). */
 typedef struct krrn_small_desc {
   const float* in;
@@ -140,9 +143,9 @@ typedef struct krrn_small_desc {
   const float* res;
   int res_cs, res_co;
   float* out;
-  int out_cs, out_co, relu, nw, ks;
+  int out_cs, out_co, relu, ksize, stride, nw, ks;
 } krrn_small_desc;
-int krrn_conv3x3_small_group_f32(const krrn_small_desc* descs, int n, void* stream);
+int krrn_conv_small_group_f32(const krrn_small_desc* descs, int n, void* stream);
 
 /* k nearest neighbours without the [n, n] distance matrix.
  * Replaces gcn3d.get_neighbor_index (gcn3d.py:15-26; mode 0, drop_first = 1: topk(k+1)[1:])

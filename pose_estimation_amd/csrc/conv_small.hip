@@ -1,12 +1,13 @@
-// Direct 3x3 / stride 1 / pad 1 convolution for the narrow HRNet branch convs (BasicBlock
-// conv1 / conv2 of the 18/36/72/144-channel branches at S/4 .. S/32, lib/network/hrnet/
-// myhrnet.py:34-63), fused with eval-BN scale / bias, the residual add and ReLU.
+// Direct convolution for the narrow HRNet convs, fused with eval-BN scale / bias, the residual add
+// and ReLU: the branch BasicBlocks' 3x3 / stride-1 convs (18/36/72/144 channels at S/4 .. S/32,
+// lib/network/hrnet/myhrnet.py:34-63) and the fuse layers' 3x3 / stride-2
+// downsamples and 1x1 projections (myhrnet.py:177-225, H4).
 //
-// These convs are tiny (0.3-0.7 GFLOP at B = 64) and were bound by per-k-tile load latency in the
-// implicit-GEMM kernel (a wave's 6-40 k-tiles each wait for an im2col gather; 21 us per launch
-// for ~3 us of matrix work). Here a block stages the input rows its 64 output pixels read — all
-// input channels, with a zero border — into LDS ONCE, and then runs the whole K = 9 x cin
-// reduction out of LDS: one global-load phase per block instead of one per k-tile.
+// These convs are tiny (0.05-0.7 GFLOP at B = 64) and were bound by per-k-tile load latency in the
+// implicit-GEMM kernel (a wave's 2-40 k-tiles each wait for an im2col gather; 13-21 us per launch
+// for ~3 us of matrix work). Here a block stages the input rows its output pixels read — all
+// input channels, with a zero border for the 3x3 ones — into LDS ONCE, and then runs the whole
+// K = taps x cin reduction out of LDS: one global-load phase per block instead of one per k-tile.
 //
 // Block = 256 threads = 4 waves = 64 consecutive output pixels in (b, y, x) raster order (any
 // number of images / rows; e.g. 4 whole 4x4 images, or 2.1 rows of a 30-wide image) x NW
@@ -27,8 +28,10 @@ namespace {
 struct SmallArgs {
   const float* in;
   int in_cs, in_co;
-  int B, H, W, cin;      // cin = physical channels (multiple of 4)
-  const float* wt;       // [N][9 * cin], k = tap * cin + c, tap = ky * 3 + kx
+  int B, H, W, cin;      // input image; cin = physical channels (multiple of 4)
+  int ksz, stride, pad;  // 3 / 1 / 1, 3 / 2 / 1 or 1 / 1 / 0
+  int Ho, Wo;            // output image
+  const float* wt;       // [N][taps * cin], k = tap * cin + c, tap = ky * ksz + kx
   int N, n_store;
   const float* scale;
   const float* bias;
@@ -37,7 +40,7 @@ struct SmallArgs {
   float* out;
   int out_cs, out_co;
   int relu;
-  int M;                 // B * H * W
+  int M;                 // B * Ho * Wo
   int q;                 // channel quads per pixel (cin / 4)
   int pitch;             // LDS float4 per staged pixel: q rounded up to odd (conflict-free reads)
 };
@@ -58,17 +61,17 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
   const int mi = wave / KS, ks = wave - (wave / KS) * KS;
   const int p0 = bx * kPixB;
   const int n0 = by * NW * 16;
-  const int HW = a.H * a.W, W2 = a.W + 2;
-  // staged rows: for each image bA..bB the input rows its output rows in [p0, p1] read (+-1)
+  const int HWo = a.Ho * a.Wo, W2 = a.W + 2 * a.pad;
+  // staged rows: for each image bA..bB the input rows its output rows in [p0, p1] read
   const int p1 = min(p0 + kPixB, a.M) - 1;
-  const int bA = p0 / HW, bB = p1 / HW;
-  const int yA = (p0 - bA * HW) / a.W, yB = (p1 - bB * HW) / a.W;
-  auto ystart = [&](int b) { return b == bA ? yA - 1 : -1; };
-  auto yend = [&](int b) { return b == bB ? yB + 1 : a.H; };  // inclusive
+  const int bA = p0 / HWo, bB = p1 / HWo;
+  const int yA = (p0 - bA * HWo) / a.Wo, yB = (p1 - bB * HWo) / a.Wo;
+  auto ystart = [&](int b) { return (b == bA ? a.stride * yA : 0) - a.pad; };
+  auto yend = [&](int b) { return (b == bB ? a.stride * yB : a.stride * (a.Ho - 1)) + a.ksz - 1 - a.pad; };  // incl.
   int nrows = 0;
   for (int b = bA; b <= bB; ++b) nrows += yend(b) - ystart(b) + 1;
 
-  // ---- stage: nrows x (W + 2) pixels x cin channels, zero outside the image -------------------
+  // ---- stage: nrows x (W + 2 pad) pixels x cin channels, zero outside the image ---------------
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + a.in_co), (short)0, (int)0x7FFFFFF0, 0x00020000);
   const int Q = a.q;
@@ -92,7 +95,7 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
         r -= yend(b) - ystart(b) + 1;
         ++b;
       }
-      const int yin = ystart(b) + r, xin = xs - 1;
+      const int yin = ystart(b) + r, xin = xs - a.pad;
       const bool ok = e < total && yin >= 0 && yin < a.H && xin >= 0 && xin < a.W;
       const unsigned off =
           ok ? (unsigned)(((((long long)b * a.H + yin) * a.W + xin) * a.in_cs + 4 * c4) * 4) : kOOB;
@@ -110,15 +113,17 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
   int base = 0;  // staged pixel of (b, y, x), the centre tap
   {
     const int mm = min(m, a.M - 1);
-    const int b = mm / HW, rr = mm - b * HW;
-    const int y = rr / a.W, x = rr - (rr / a.W) * a.W;
+    const int b = mm / HWo, rr = mm - b * HWo;
+    const int y = rr / a.Wo, x = rr - (rr / a.Wo) * a.Wo;
     int rowslot = 0;
     for (int bb = bA; bb < b; ++bb) rowslot += yend(bb) - ystart(bb) + 1;
-    rowslot += y - ystart(b);
-    base = rowslot * W2 + x + 1;
+    rowslot += a.stride * y - ystart(b);
+    base = rowslot * W2 + a.stride * x + a.pad;
   }
-  const int K = 9 * a.cin;
-  const int KQ = 9 * Q;  // k-quads
+  const int taps = a.ksz * a.ksz;
+  const int tb = a.ksz == 1 ? 4 : 0;  // a 1x1 conv's one tap is the 3x3 grid's centre
+  const int K = taps * a.cin;
+  const int KQ = taps * Q;  // k-quads
   const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.wt, (short)0, (int)min((long long)a.N * K * 4, (long long)kOOB), 0x00020000);
   unsigned wrow[NW];
@@ -165,9 +170,10 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
 #pragma unroll
       for (int j = 0; j < NW; ++j) w[j] = wr[u][j];
       wload(st + PF, wr[u]);
-      const int ty = tap >= 6 ? 1 : (tap >= 3 ? 0 : -1);
-      const int tx = tap - 3 * (ty + 1) - 1;
-      const bool kok = tap < 9;
+      const int t3 = tap + tb;
+      const int ty = t3 >= 6 ? 1 : (t3 >= 3 ? 0 : -1);
+      const int tx = t3 - 3 * (ty + 1) - 1;
+      const bool kok = tap < taps;
       const int px = kok ? base + ty * W2 + tx : base;
       f32x4 av = *reinterpret_cast<const f32x4*>(slab + 4 * (px * a.pitch + c4));
       if (!kok) av = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -224,7 +230,7 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
 }
 
 template <int NW, int KS>
-__global__ __launch_bounds__(256) void conv3x3_small_kernel(const SmallArgs a) {
+__global__ __launch_bounds__(256) void conv_small_kernel(const SmallArgs a) {
   extern __shared__ __attribute__((aligned(16))) float slab[];
   small_body<NW, KS>(a, blockIdx.x, blockIdx.y, slab);
 }
@@ -242,7 +248,7 @@ struct SmallGroup {
   int n;
 };
 
-__global__ __launch_bounds__(256) void conv3x3_small_group_kernel(const SmallGroup g) {
+__global__ __launch_bounds__(256) void conv_small_group_kernel(const SmallGroup g) {
   extern __shared__ __attribute__((aligned(16))) float slab[];
   const int blk = blockIdx.x;
   int i = 0;
@@ -263,25 +269,26 @@ __global__ __launch_bounds__(256) void conv3x3_small_group_kernel(const SmallGro
 }
 
 // LDS floats of the largest slab any block of this problem stages (host mirror of the kernel's
-// row count: the rows of the images a block's pixel range touches, +-1)
-long long slab_floats(int B, int H, int W, int pitch, int pixb) {
-  const long long HW = (long long)H * W, M = (long long)B * HW;
+// row count: the input rows of the output rows a block's pixel range covers)
+long long slab_floats(const SmallArgs& a, int pixb) {
+  const long long HWo = (long long)a.Ho * a.Wo, M = (long long)a.B * HWo;
   long long worst = 0;
   for (long long p0 = 0; p0 < M; p0 += pixb) {
     const long long p1 = (p0 + pixb < M ? p0 + pixb : M) - 1;
-    const long long bA = p0 / HW, bB = p1 / HW;
-    const long long yA = (p0 - bA * HW) / W, yB = (p1 - bB * HW) / W;
+    const long long bA = p0 / HWo, bB = p1 / HWo;
+    const long long yA = (p0 - bA * HWo) / a.Wo, yB = (p1 - bB * HWo) / a.Wo;
     long long rows = 0;
-    for (long long b = bA; b <= bB; ++b) rows += (b == bB ? yB + 1 : H) - (b == bA ? yA - 1 : -1) + 1;
+    for (long long b = bA; b <= bB; ++b)
+      rows += (b == bB ? a.stride * yB : a.stride * (a.Ho - 1)) + a.ksz - 1 - (b == bA ? a.stride * yA : 0) + 1;
     if (rows > worst) worst = rows;
-    if (p0 >= (long long)pixb * HW) break;  // block starts repeat modulo lcm(pixb, HW)
+    if (p0 >= (long long)pixb * HWo) break;  // block starts repeat modulo lcm(pixb, HWo)
   }
-  return worst * (W + 2) * pitch * 4;
+  return worst * (a.W + 2 * a.pad) * a.pitch * 4;
 }
 
 // dynamic LDS bytes of one (NW, KS) launch: the slab, or the K-slice partials if larger
 long long small_lds(const SmallArgs& a, int nw, int ks) {
-  long long lds = slab_floats(a.B, a.H, a.W, a.pitch, 64 / ks) * 4;
+  long long lds = slab_floats(a, 64 / ks) * 4;
   const long long red = 4LL * nw * 64 * 4 * 4;
   if (ks > 1 && lds < red) lds = red;
   return lds;
@@ -300,25 +307,31 @@ template <int NW, int KS>
 int small_launch(const SmallArgs& a, hipStream_t s) {
   constexpr int pixb = 64 / KS;
   const long long lds = small_lds(a, NW, KS);
-  const int st = set_lds((const void*)conv3x3_small_kernel<NW, KS>, lds);
+  const int st = set_lds((const void*)conv_small_kernel<NW, KS>, lds);
   if (st != KRRN_OK) return st;
   const dim3 grid(krrn_cdiv(a.M, pixb), krrn_cdiv(krrn_cdiv(a.N, 16), NW));
-  hipLaunchKernelGGL((conv3x3_small_kernel<NW, KS>), grid, dim3(256), (size_t)lds, s, a);
+  hipLaunchKernelGGL((conv_small_kernel<NW, KS>), grid, dim3(256), (size_t)lds, s, a);
   return krrn_launch_status();
 }
 
 int make_args(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* wt, int N,
               int n_store, const float* scale, const float* bias, const float* res, int res_cs, int res_co,
-              float* out, int out_cs, int out_co, int relu, int nw, int ks, SmallArgs& a) {
+              float* out, int out_cs, int out_co, int relu, int ksize, int stride, int nw, int ks, SmallArgs& a) {
   if (!in || !wt || !out) return KRRN_EARG;
   if (B < 1 || H < 1 || W < 1 || N < 1 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
   if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
   if (!krrn_aligned16(in) || !krrn_aligned16(wt)) return KRRN_EALIGN;
   if (out_co + n_store > out_cs || (res && res_co + n_store > res_cs)) return KRRN_ESHAPE;
   if (nw < 1 || nw > 3 || (ks != 1 && ks != 2 && ks != 4)) return KRRN_EARG;
-  const long long M = (long long)B * H * W;
-  if (M > 0x7fffffffLL || M * in_cs * 4 >= 0x7FFFFFF0LL || (long long)N * 9 * cin * 4 >= (long long)kOOB)
+  if ((ksize != 1 && ksize != 3) || (stride != 1 && stride != 2)) return KRRN_EARG;
+  const int pad = (ksize - 1) / 2;
+  const int Ho = (H + 2 * pad - ksize) / stride + 1, Wo = (W + 2 * pad - ksize) / stride + 1;
+  if (Ho < 1 || Wo < 1) return KRRN_ESHAPE;
+  const long long M = (long long)B * Ho * Wo;
+  if (M > 0x7fffffffLL || (long long)B * H * W * in_cs * 4 >= 0x7FFFFFF0LL ||
+      (long long)N * ksize * ksize * cin * 4 >= (long long)kOOB)
     return KRRN_ESHAPE;
+  a.ksz = ksize; a.stride = stride; a.pad = pad; a.Ho = Ho; a.Wo = Wo;
   a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = H; a.W = W; a.cin = cin;
   a.wt = wt; a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
   a.res = res; a.res_cs = res_cs; a.res_co = res_co; a.out = out; a.out_cs = out_cs; a.out_co = out_co;
@@ -330,13 +343,13 @@ int make_args(const float* in, int in_cs, int in_co, int B, int H, int W, int ci
 
 }  // namespace
 
-KRRN_API int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
-                                    const float* wt, int N, int n_store, const float* scale, const float* bias,
-                                    const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
-                                    int relu, int nw, int ks, void* stream) {
+KRRN_API int krrn_conv_small_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* wt,
+                                 int N, int n_store, const float* scale, const float* bias, const float* res,
+                                 int res_cs, int res_co, float* out, int out_cs, int out_co, int relu, int ksize,
+                                 int stride, int nw, int ks, void* stream) {
   SmallArgs a;
   const int st = make_args(in, in_cs, in_co, B, H, W, cin, wt, N, n_store, scale, bias, res, res_cs, res_co, out,
-                           out_cs, out_co, relu, nw, ks, a);
+                           out_cs, out_co, relu, ksize, stride, nw, ks, a);
   if (st != KRRN_OK) return st;
   hipStream_t s = (hipStream_t)stream;
 #define KRRN_SMALL(NWV, KSV) \
@@ -348,7 +361,7 @@ KRRN_API int krrn_conv3x3_small_f32(const float* in, int in_cs, int in_co, int B
   return KRRN_EARG;
 }
 
-KRRN_API int krrn_conv3x3_small_group_f32(const krrn_small_desc* d, int n, void* stream) {
+KRRN_API int krrn_conv_small_group_f32(const krrn_small_desc* d, int n, void* stream) {
   if (!d || n < 1 || n > kSmallMaxGroup) return KRRN_EARG;
   SmallGroup g;
   long long blocks[kSmallMaxGroup], lds = 0;
@@ -357,14 +370,17 @@ KRRN_API int krrn_conv3x3_small_group_f32(const krrn_small_desc* d, int n, void*
     SmallArgs& a = g.a[i];
     const krrn_small_desc& q = d[i];
     const int st = make_args(q.in, q.in_cs, q.in_co, q.B, q.H, q.W, q.cin, q.wt, q.N, q.n_store, q.scale, q.bias,
-                             q.res, q.res_cs, q.res_co, q.out, q.out_cs, q.out_co, q.relu, q.nw, q.ks, a);
+                             q.res, q.res_cs, q.res_co, q.out, q.out_cs, q.out_co, q.relu, q.ksize, q.stride, q.nw,
+                             q.ks, a);
     if (st != KRRN_OK) return st;
     const long long l = small_lds(a, q.nw, q.ks);
     if (l > lds) lds = l;
     order[i] = i;
   }
   // longest block first: per-block MFMA steps ~ ceil(9 cin / 16) / ks x nw tiles
-  auto cost = [&](int i) { return (long long)((9 * d[i].cin + 15) / 16 + d[i].ks - 1) / d[i].ks * d[i].nw; };
+  auto cost = [&](int i) {
+    return (long long)((d[i].ksize * d[i].ksize * d[i].cin + 15) / 16 + d[i].ks - 1) / d[i].ks * d[i].nw;
+  };
   for (int i = 1; i < n; ++i)
     for (int j = i; j > 0 && cost(order[j]) > cost(order[j - 1]); --j) {
       const int t = order[j];
@@ -386,8 +402,8 @@ KRRN_API int krrn_conv3x3_small_group_f32(const krrn_small_desc* d, int n, void*
   }
   h.start[n] = (int)total;
   if (total > 0x7fffffffLL) return KRRN_ESHAPE;
-  const int st = set_lds((const void*)conv3x3_small_group_kernel, lds);
+  const int st = set_lds((const void*)conv_small_group_kernel, lds);
   if (st != KRRN_OK) return st;
-  hipLaunchKernelGGL(conv3x3_small_group_kernel, dim3((unsigned)total), dim3(256), (size_t)lds, (hipStream_t)stream, h);
+  hipLaunchKernelGGL(conv_small_group_kernel, dim3((unsigned)total), dim3(256), (size_t)lds, (hipStream_t)stream, h);
   return krrn_launch_status();
 }

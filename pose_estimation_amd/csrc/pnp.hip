@@ -413,6 +413,7 @@ __device__ __forceinline__ void alphas_of(const double* p, const double cws[4][3
 }
 
 __device__ __forceinline__ void gauss_newton(const double (&L)[60], const double (&rho)[6], double (&betas)[4]) {
+#pragma unroll 1
   for (int it = 0; it < 5; ++it) {
     double A[24], b[6], x[4];
 #pragma unroll
@@ -635,6 +636,7 @@ __device__ void epnp(const SUM& sum, const Pts& P, const Cam& cam, double (&Rout
     }
   }
   double best_err = 1e300;
+#pragma unroll 1
   for (int approx = 1; approx <= 3; ++approx) {
     double betas[4] = {0, 0, 0, 0};
     if (approx == 1) {

@@ -231,26 +231,27 @@ class _Builder:
 
     @staticmethod
     def small_problem(x: Act, spec, out: Act, res: Optional[Act], relu: bool) -> dict:
-        """krrn_conv3x3_small_f32's arguments (SmallDesc fields) plus the breakdown's FLOP counts."""
+        """krrn_conv_small_f32's arguments (SmallDesc fields) plus the breakdown's FLOP counts."""
         np_ = pad4(spec.cout)
         M = x.B * out.H * out.W
+        taps = spec.ksize * spec.ksize
         ntiles = (np_ + 15) // 16
         nw, ks = ops.small_conv_config(M, ntiles, spec.cin_p)
         return dict(x=ptr(x.t), in_cs=x.cs, in_co=x.co, B=x.B, H=x.H, W=x.W, cin=spec.cin_p, wt=ptr(spec.wt[0]),
                     N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
                     res=ptr(res.t) if res is not None else ptr(None), res_cs=res.cs if res is not None else 0,
                     res_co=res.co if res is not None else 0, out=ptr(out.t), out_cs=out.cs, out_co=out.co,
-                    relu=int(relu), nw=nw, ks=ks, flops=2.0 * spec.cin * spec.cout * 9 * M,
-                    mfma_flops=2.0 * 16 * ((9 * spec.cin_p // 4 + 3) // 4) * 16 * ntiles * M)
+                    relu=int(relu), ksize=spec.ksize, stride=spec.stride, nw=nw, ks=ks, M=M,
+                    flops=2.0 * spec.cin * spec.cout * taps * M,
+                    mfma_flops=2.0 * 16 * ((taps * spec.cin_p // 4 + 3) // 4) * 16 * ntiles * M)
 
     def emit_small(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         p = self.small_problem(x, spec, out, res, relu)
-        M = x.B * out.H * out.W
-        self.plan.add("krrn_conv3x3_small_f32", p["x"], p["in_cs"], p["in_co"], p["B"], p["H"], p["W"], p["cin"], p["wt"],
+        self.plan.add("krrn_conv_small_f32", p["x"], p["in_cs"], p["in_co"], p["B"], p["H"], p["W"], p["cin"], p["wt"],
                       p["N"], p["n_store"], p["scale"], p["bias"], p["res"], p["res_cs"], p["res_co"], p["out"],
-                      p["out_cs"], p["out_co"], p["relu"], p["nw"], p["ks"],
-                      meta=dict(kernel=f"conv3x3_small<{p['nw']},{p['ks']}>", flops=p["flops"], tag=tag, M=M, N=p["N"],
-                                K=spec.cin_p * 9, splits=1, mfma_flops=p["mfma_flops"]))
+                      p["out_cs"], p["out_co"], p["relu"], p["ksize"], p["stride"], p["nw"], p["ks"],
+                      meta=dict(kernel=f"conv_small<{p['nw']},{p['ks']}>", flops=p["flops"], tag=tag, M=p["M"], N=p["N"],
+                                K=spec.cin_p * spec.ksize ** 2, splits=1, mfma_flops=p["mfma_flops"]))
 
     def emit_wino(self, x: Act, spec, U: torch.Tensor, out: Act, res: Optional[Act], relu: bool,
                   tag: str = "conv"):
@@ -291,7 +292,7 @@ class _Builder:
 
     def small_grouped(self, xs: List[Act], convs: List[Tuple[nn.Module, nn.Module]], res: Optional[List[Act]],
                       tag: str) -> Optional[List[Act]]:
-        """The i-th conv on xs[i] for every branch as ONE krrn_conv3x3_small_group_f32 launch, or
+        """The i-th conv on xs[i] for every branch as ONE krrn_conv_small_group_f32 launch, or
         None (nothing emitted) when one of them is not a small-conv problem."""
         specs = []
         for x, (conv, bn) in zip(xs, convs):

@@ -238,7 +238,7 @@ def wino_eligible(spec: ConvSpec, M: int) -> bool:
 
 
 def small_conv_config(M: int, ntiles: int, cin_p: int):
-    """(nw, ks) for krrn_conv3x3_small_f32 from the branch-conv sweep (profiles/bench_branch_conv.py,
+    """(nw, ks) for krrn_conv_small_f32 from the branch-conv sweep (profiles/bench_branch_conv.py,
     W18 at B = 64): 30x30x20 (2, 1) 17.5 us, 15x15x36 (3, 2) 12.7 us, 8x8x72 (3, 4) 12.7 us, 4x4x144
     (3, 4) 14.2 us, against 18.4 / 15.5 / 17.9 / 17.3 us for the best implicit-GEMM tile / split-K.
     Large M: whole reductions per wave; small M: the reduction split over the block's waves."""
@@ -248,22 +248,32 @@ def small_conv_config(M: int, ntiles: int, cin_p: int):
 
 
 def small_conv_eligible(spec: ConvSpec, x) -> bool:
-    """krrn_conv3x3_small_f32: narrow 3x3 / stride 1 / pad 1 convs (the HRNet branches' BasicBlocks,
-    up to 160 input channels) whose 64-pixel blocks' input rows fit the LDS."""
-    if not (spec.kind == "conv" and spec.ksize == 3 and spec.stride == 1 and spec.pad == 1):
+    """krrn_conv_small_f32: narrow convs whose 64-pixel blocks' input rows fit the LDS (up to 256
+    physical input channels): every 3x3 / stride-1 / pad-1 conv (the HRNet branches' BasicBlocks),
+    and the latency-bound 3x3 / stride-2 and 1x1 convs of the fuse layers and transitions (output
+    M <= 16384 pixels or <= 32 channels; the stem and layer1's wide ones stay on the implicit GEMM)."""
+    if spec.kind != "conv":
+        return False
+    k, st, pad = spec.ksize, spec.stride, spec.pad
+    if not ((k == 3 and pad == 1 and st in (1, 2)) or (k == 1 and pad == 0 and st == 1)):
         return False
     if spec.cin_p > 256 or x.co % 4 or x.cs % 4:
         return False
+    Ho, Wo = conv_out_hw(spec, x.H, x.W)
+    HWo = Ho * Wo
+    M = x.B * HWo
+    if not (k == 3 and st == 1) and not (M <= 16384 or spec.cout <= 32):
+        return False
     pitch = (spec.cin_p // 4) | 1
-    HW = x.H * x.W
     rows = 0
-    for p0 in range(0, min(x.B * HW, 64 * HW), 16):  # block starts repeat modulo lcm(pixb, HW)
-        p1 = min(p0 + 64, x.B * HW) - 1
-        bA, bB = p0 // HW, p1 // HW
-        yA, yB = (p0 - bA * HW) // x.W, (p1 - bB * HW) // x.W
-        r = sum(((yB + 1) if b == bB else x.H) - ((yA - 1) if b == bA else -1) + 1 for b in range(bA, bB + 1))
+    for p0 in range(0, min(M, 64 * HWo), 16):  # block starts repeat modulo lcm(pixb, HWo)
+        p1 = min(p0 + 64, M) - 1
+        bA, bB = p0 // HWo, p1 // HWo
+        yA, yB = (p0 - bA * HWo) // Wo, (p1 - bB * HWo) // Wo
+        r = sum(((st * yB) if b == bB else st * (Ho - 1)) + k - 1 - ((st * yA) if b == bA else 0) + 1
+                for b in range(bA, bB + 1))
         rows = max(rows, r)
-    return rows * (x.W + 2) * pitch * 16 <= 96 * 1024
+    return rows * (x.W + 2 * pad) * pitch * 16 <= 96 * 1024
 
 
 def make_convT(convT: torch.nn.ConvTranspose2d, bn: Optional[torch.nn.Module], device,

@@ -44,8 +44,8 @@ _lib.register("krrn_rng_advance", [P, P])
 _lib.register("krrn_conv2d_group_f32", [P, I, I, P])
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_wino_variant", [I])
-_lib.register("krrn_conv3x3_small_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, I, I, P])
-_lib.register("krrn_conv3x3_small_group_f32", [P, I, P])
+_lib.register("krrn_conv_small_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, I, I, I, I, P])
+_lib.register("krrn_conv_small_group_f32", [P, I, P])
 _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L, P, P])
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])
@@ -292,14 +292,14 @@ GROUP_TILE = int(os.environ.get("KRRN_GROUP_TILE", "6"))
 
 
 class SmallDesc(ctypes.Structure):
-    """krrn_small_desc (include/krrn_hip.h): the arguments of krrn_conv3x3_small_f32."""
+    """krrn_small_desc (include/krrn_hip.h): the arguments of krrn_conv_small_f32."""
     _fields_ = [("in_", P), ("in_cs", I), ("in_co", I), ("B", I), ("H", I), ("W", I), ("cin", I), ("wt", P), ("N", I),
                 ("n_store", I), ("scale", P), ("bias", P), ("res", P), ("res_cs", I), ("res_co", I), ("out", P),
-                ("out_cs", I), ("out_co", I), ("relu", I), ("nw", I), ("ks", I)]
+                ("out_cs", I), ("out_co", I), ("relu", I), ("ksize", I), ("stride", I), ("nw", I), ("ks", I)]
 
 
 def add_small_group(plan: Plan, problems: List[dict], tag: str = "small_group"):
-    """One krrn_conv3x3_small_group_f32 launch over up to 4 independent small convs (dicts of
+    """One krrn_conv_small_group_f32 launch over up to 4 independent small convs (dicts of
     SmallDesc fields, `in_` as `x`, plus 'flops' / 'mfma_flops' for the breakdown)."""
     n = len(problems)
     arr = (SmallDesc * n)()
@@ -311,10 +311,10 @@ def add_small_group(plan: Plan, problems: List[dict], tag: str = "small_group"):
         mfma += pr.pop("mfma_flops")
         pr["in_"] = pr.pop("x")
         arr[q] = SmallDesc(**pr)
-        shapes.append((pr["B"] * pr["H"] * pr["W"], pr["N"], 9 * pr["cin"], 1))
+        shapes.append((pr.pop("M"), pr["N"], pr["ksize"] ** 2 * pr["cin"], 1))
     plan.buffers.append(arr)
-    plan.add("krrn_conv3x3_small_group_f32", ctypes.cast(arr, P), n,
-             meta=dict(kernel="conv3x3_small_group", flops=flops, tag=tag, M=shapes[0][0], N=shapes[0][1],
+    plan.add("krrn_conv_small_group_f32", ctypes.cast(arr, P), n,
+             meta=dict(kernel="conv_small_group", flops=flops, tag=tag, M=shapes[0][0], N=shapes[0][1],
                        K=shapes[0][2], splits=1, shapes=shapes, mfma_flops=mfma))
 
 

@@ -63,8 +63,8 @@ for cp, c, H in shapes:
     for nw in [int(v) for v in os.environ.get("SMALL_NW", "1,2,3").split(",") if v]:
         for ks in [int(v) for v in os.environ.get("SMALL_KS", "1,2,4").split(",") if v]:
             def run_small():
-                _lib.check(L.krrn_conv3x3_small_f32(ptr(xd), cp, 0, B, H, H, cp, ptr(wd), cp, cp, P(0), P(0), P(0), 0,
-                                                    0, ptr(out), cp, 0, 0, nw, ks, st), "small conv")
+                _lib.check(L.krrn_conv_small_f32(ptr(xd), cp, 0, B, H, H, cp, ptr(wd), cp, cp, P(0), P(0), P(0), 0,
+                                                    0, ptr(out), cp, 0, 0, 3, 1, nw, ks, st), "small conv")
             ms = ev_time(run_small)
             err = float((out.cpu() - ref).abs().max())
             print(f"C{c:3d} {H:2d}x{H:2d} small nw {nw} ks {ks}: {ms*1e3:7.1f} us {fl/ms/1e9:6.1f} TF err {err:.1e}",

@@ -1,6 +1,6 @@
 """Micro-bench: the four W18 stage-4 branch convs (18/36/72/144 channels at S/4 .. S/32, B = 64) as
-four krrn_conv3x3_small_f32 launches on one stream, on four streams, and as one
-krrn_conv3x3_small_group_f32 launch; each variant repeated `DEPTH` times back to back (a module's
+four krrn_conv_small_f32 launches on one stream, on four streams, and as one
+krrn_conv_small_group_f32 launch; each variant repeated `DEPTH` times back to back (a module's
 block chain).
 
 usage (GPU box): python3 profiles/bench_small_group.py
@@ -32,15 +32,15 @@ streams = [torch.cuda.Stream(dev) for _ in shapes]
 
 
 def single(p, st):
-    _lib.check(L.krrn_conv3x3_small_f32(ptr(p["x"]), p["cp"], 0, B, p["H"], p["H"], p["cp"], ptr(p["w"]), p["cp"],
-                                        p["cp"], P(0), P(0), P(0), 0, 0, ptr(p["out"]), p["cp"], 0, 1, p["nw"],
+    _lib.check(L.krrn_conv_small_f32(ptr(p["x"]), p["cp"], 0, B, p["H"], p["H"], p["cp"], ptr(p["w"]), p["cp"],
+                                        p["cp"], P(0), P(0), P(0), 0, 0, ptr(p["out"]), p["cp"], 0, 1, 3, 1, p["nw"],
                                         p["ks"], P(st.cuda_stream)), "small")
 
 
 arr = (SmallDesc * len(probs))(*[SmallDesc(in_=ptr(p["x"]), in_cs=p["cp"], in_co=0, B=B, H=p["H"], W=p["H"],
                                            cin=p["cp"], wt=ptr(p["w"]), N=p["cp"], n_store=p["cp"], scale=P(0),
                                            bias=P(0), res=P(0), res_cs=0, res_co=0, out=ptr(p["out"]),
-                                           out_cs=p["cp"], out_co=0, relu=1, nw=p["nw"], ks=p["ks"])
+                                           out_cs=p["cp"], out_co=0, relu=1, ksize=3, stride=1, nw=p["nw"], ks=p["ks"])
                                  for p in probs])
 
 
@@ -65,7 +65,7 @@ def run_streams():
 def run_group():
     st = torch.cuda.current_stream()
     for _ in range(DEPTH):
-        _lib.check(L.krrn_conv3x3_small_group_f32(ctypes.cast(arr, P), len(probs), P(st.cuda_stream)), "group")
+        _lib.check(L.krrn_conv_small_group_f32(ctypes.cast(arr, P), len(probs), P(st.cuda_stream)), "group")
 
 
 def graph_time(fn, reps=20):

@@ -224,33 +224,40 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
-@pytest.mark.parametrize("B,cin,cout,H,W,co,nw,ks", [(3, 20, 18, 30, 30, 0, 2, 1), (64, 144, 144, 4, 4, 0, 1, 4),
-                                                     (8, 36, 36, 15, 15, 4, 3, 2), (5, 72, 72, 8, 8, 0, 1, 4),
-                                                     (2, 12, 40, 7, 9, 0, 2, 2), (3, 4, 8, 5, 6, 0, 1, 1)])
-def test_conv3x3_small(dev, B, cin, cout, H, W, co, nw, ks):
-    """LDS-staged direct 3x3 conv (the HRNet branch BasicBlock convs): blocks spanning several
-    images / rows, channel-offset input, residual + ReLU, partial 16-channel tiles, vs torch fp32."""
+@pytest.mark.parametrize("B,cin,cout,H,W,co,nw,ks,k,st", [
+    (3, 20, 18, 30, 30, 0, 2, 1, 3, 1), (64, 144, 144, 4, 4, 0, 1, 4, 3, 1), (8, 36, 36, 15, 15, 4, 3, 2, 3, 1),
+    (5, 72, 72, 8, 8, 0, 1, 4, 3, 1), (2, 12, 40, 7, 9, 0, 2, 2, 3, 1), (3, 4, 8, 5, 6, 0, 1, 1, 3, 1),
+    # the fuse layers' stride-2 downsamples (odd and even sizes) and 1x1 projections
+    (4, 20, 36, 30, 30, 0, 3, 2, 3, 2), (3, 36, 72, 15, 15, 0, 3, 4, 3, 2), (6, 72, 144, 8, 8, 4, 3, 4, 3, 2),
+    (2, 20, 20, 7, 9, 0, 2, 1, 3, 2), (5, 36, 20, 15, 15, 0, 2, 2, 1, 1), (7, 144, 72, 4, 4, 4, 3, 4, 1, 1),
+    (2, 72, 36, 8, 8, 0, 3, 1, 1, 1)])
+def test_conv_small(dev, B, cin, cout, H, W, co, nw, ks, k, st):
+    """LDS-staged direct conv (HRNet branch BasicBlocks, fuse-layer downsamples / projections):
+    blocks spanning several images / rows, channel-offset input, residual + ReLU, partial
+    16-channel tiles, vs torch fp32."""
     from pose_estimation_amd import _lib
     from pose_estimation_amd.runtime import P, ptr
-    g = torch.Generator().manual_seed(cin * cout + H)
-    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+    g = torch.Generator().manual_seed(cin * cout + H + 7 * k + st)
+    conv = nn.Conv2d(cin, cout, k, st, (k - 1) // 2, bias=False)
     with torch.no_grad():
         conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
     bn = _bn(cout, g)
     x = torch.randn(B, cin, H, W, generator=g)
-    res = torch.randn(B, cout, H, W, generator=g)
-    ref = torch.relu(bn(conv(x)) + res).detach()
+    y = bn(conv(x)).detach()
+    Ho, Wo = y.shape[2], y.shape[3]
+    res = torch.randn(B, cout, Ho, Wo, generator=g)
+    ref = torch.relu(y + res)
     cs = ops.pad4(cin) + co + 4
     xa = _nhwc(x, dev, cs=cs, co=co)
     spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
     ra = _nhwc(res, dev)
     np_ = ops.pad4(cout)
-    out = ops.new_act(B, H, W, cout, dev, cs=np_ + 4)
+    out = ops.new_act(B, Ho, Wo, cout, dev, cs=np_ + 4)
     out.t.fill_(float("nan"))
     out.t[..., np_:] = 0.0
-    _lib.check(_lib.lib().krrn_conv3x3_small_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(spec.wt[0]), np_,
-                                                 np_, ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
-                                                 out.cs, 0, 1, nw, ks, P(torch.cuda.current_stream().cuda_stream)),
+    _lib.check(_lib.lib().krrn_conv_small_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(spec.wt[0]), np_,
+                                              np_, ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
+                                              out.cs, 0, 1, k, st, nw, ks, P(torch.cuda.current_stream().cuda_stream)),
                "small conv")
     torch.cuda.synchronize()
     got = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
@@ -258,9 +265,9 @@ def test_conv3x3_small(dev, B, cin, cout, H, W, co, nw, ks):
     assert torch.count_nonzero(out.t[..., np_:]).item() == 0
 
 
-def test_conv3x3_small_group(dev):
-    """krrn_conv3x3_small_group_f32: the four W18 branch shapes (and their (nw, ks) configs) in one
-    launch give exactly the single launches' outputs."""
+def test_conv_small_group(dev):
+    """krrn_conv_small_group_f32: the four W18 branch shapes (and their (nw, ks) configs) plus a
+    stride-2 and a 1x1 problem in one launch give exactly the single launches' outputs."""
     from pose_estimation_amd import _lib
     from pose_estimation_amd.runtime import P, SmallDesc, ptr
     import ctypes
@@ -268,28 +275,32 @@ def test_conv3x3_small_group(dev):
     st = P(torch.cuda.current_stream().cuda_stream)
     B = 6
     g = torch.Generator().manual_seed(7)
-    descs, singles = [], []
-    for cin, H, nw, ks in [(18, 30, 2, 1), (36, 15, 3, 2), (72, 8, 3, 4), (144, 4, 3, 4)]:
-        cp = ops.pad4(cin)
-        conv = nn.Conv2d(cin, cin, 3, 1, 1, bias=False)
-        with torch.no_grad():
-            conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
-        spec = ops.make_conv(conv, _bn(cin, g), dev, cin_p=cp)
-        xa = _nhwc(torch.randn(B, cin, H, H, generator=g), dev)
-        ra = _nhwc(torch.randn(B, cin, H, H, generator=g), dev)
-        outs = [torch.full((B, H, H, cp), float("nan"), device=dev) for _ in range(2)]
-        args = dict(in_=ptr(xa.t), in_cs=xa.cs, in_co=0, B=B, H=H, W=H, cin=cp, wt=ptr(spec.wt[0]), N=cp, n_store=cp,
-                    scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(ra.t), res_cs=ra.cs, res_co=0, out_cs=cp,
-                    out_co=0, relu=1, nw=nw, ks=ks)
-        descs.append(SmallDesc(out=ptr(outs[0]), **args))
-        a = dict(args, out=ptr(outs[1]))
-        _lib.check(L.krrn_conv3x3_small_f32(a["in_"], a["in_cs"], 0, B, H, H, cp, a["wt"], cp, cp, a["scale"],
-                                            a["bias"], a["res"], a["res_cs"], 0, a["out"], cp, 0, 1, nw, ks, st),
-                   "small conv")
-        singles.append((outs, spec, xa, ra))
-    arr = (SmallDesc * len(descs))(*descs)
-    _lib.check(L.krrn_conv3x3_small_group_f32(ctypes.cast(arr, P), len(descs), st), "small group")
-    torch.cuda.synchronize()
-    for outs, *_ in singles:
-        assert not torch.isnan(outs[0]).any()
-        assert torch.equal(outs[0], outs[1])
+    for shapes in ([(18, 18, 30, 2, 1, 3, 1), (36, 36, 15, 3, 2, 3, 1), (72, 72, 8, 3, 4, 3, 1),
+                    (144, 144, 4, 3, 4, 3, 1)],
+                   [(20, 36, 30, 3, 2, 3, 2), (72, 20, 8, 2, 4, 1, 1), (36, 72, 15, 3, 4, 3, 2)]):
+        descs, singles = [], []
+        for cin, cout, H, nw, ks, k, s2 in shapes:
+            cp, np_ = ops.pad4(cin), ops.pad4(cout)
+            conv = nn.Conv2d(cin, cout, k, s2, (k - 1) // 2, bias=False)
+            with torch.no_grad():
+                conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
+            spec = ops.make_conv(conv, _bn(cout, g), dev, cin_p=cp)
+            Ho = (H + 2 * ((k - 1) // 2) - k) // s2 + 1
+            xa = _nhwc(torch.randn(B, cin, H, H, generator=g), dev)
+            ra = _nhwc(torch.randn(B, cout, Ho, Ho, generator=g), dev)
+            outs = [torch.full((B, Ho, Ho, np_), float("nan"), device=dev) for _ in range(2)]
+            args = dict(in_=ptr(xa.t), in_cs=xa.cs, in_co=0, B=B, H=H, W=H, cin=cp, wt=ptr(spec.wt[0]), N=np_,
+                        n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(ra.t), res_cs=ra.cs,
+                        res_co=0, out_cs=np_, out_co=0, relu=1, ksize=k, stride=s2, nw=nw, ks=ks)
+            descs.append(SmallDesc(out=ptr(outs[0]), **args))
+            a = dict(args, out=ptr(outs[1]))
+            _lib.check(L.krrn_conv_small_f32(a["in_"], a["in_cs"], 0, B, H, H, cp, a["wt"], np_, np_, a["scale"],
+                                             a["bias"], a["res"], a["res_cs"], 0, a["out"], np_, 0, 1, k, s2, nw, ks,
+                                             st), "small conv")
+            singles.append((outs, spec, xa, ra))
+        arr = (SmallDesc * len(descs))(*descs)
+        _lib.check(L.krrn_conv_small_group_f32(ctypes.cast(arr, P), len(descs), st), "small group")
+        torch.cuda.synchronize()
+        for outs, *_ in singles:
+            assert not torch.isnan(outs[0]).any()
+            assert torch.equal(outs[0], outs[1])
