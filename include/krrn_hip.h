@@ -102,6 +102,14 @@ int krrn_blas_gemm_run(const krrn_blas_gemm* g, const float* a, const float* w, 
                        float* out, void* workspace, long long ws_bytes, void* stream);
 int krrn_blas_gemm_destroy(krrn_blas_gemm* g);
 
+/* 1x1 conv with NCHW output (the heads' final xyz / normal convs, lib/network/krrn.py:97-98,
+ * 80-84): out[b][out_co + n][p] = scale[n] * sum_c in[(b * HW + p) * in_cs + in_co + c] wt[n][c]
+ * + bias[n] for n < n_store, p < HW; out has out_cs channels per image. cin <= 256 (multiple of 4),
+ * N <= 80 weight rows (wt [N][cin]); in / wt 16-byte aligned. */
+int krrn_conv1x1_nchw_f32(const float* in, int in_cs, int in_co, int B, int HW, int cin, const float* wt, int N,
+                          int n_store, const float* scale, const float* bias, float* out, int out_cs, int out_co,
+                          void* stream);
+
 /* 3x3 stride-1 pad-1 convolution by fused Winograd F(2x2, 3x3) (the head / last_layer /
  * deconv-BasicBlock convs: krrn.py:46-84, myhrnet.py:324-346; cuDNN / MIOpen use the same
  * algorithm for these f32 convs). U = G g G^T are the transformed weights, f32 in chunk-major

@@ -387,7 +387,7 @@ class FusionNetLite(nn.Module):
         feat = torch.cat([indexing_neighbor(fm_5, nn2).squeeze(2), indexing_neighbor(feat_1, nn1).squeeze(2),
                           indexing_neighbor(feat_2, nn1).squeeze(2)], 2)
         if trace is not None:
-            trace.update(idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1[..., 0], nn2=nn2[..., 0], feat1=feat_1,
+            trace.update(idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1[..., 0], nn2=nn2[..., 0], feat1=feat_1, p9=feat_feature,
                          feat2=feat_2, fm5=fm_5, pool_1=pool_1, pool_2=pool_2, perms=used,
                          pool_v=self.pool_1_v.last_idx, pool_x=self.pool_1_x.last_idx,
                          pool_n=self.pool_1_n.last_idx, pool2=self.pool_2.last_idx)

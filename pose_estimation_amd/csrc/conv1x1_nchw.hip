@@ -1,0 +1,135 @@
+// The heads' final 1x1 convs with NCHW output: xyz_final (128 -> mask | region | xyz logits, 72
+// channels for one class) and nml_final (128 -> 3 C normals), lib/network/krrn.py:97-98 / 80-84,
+// SURVEY §8a D1 / D2. The API returns NCHW maps, so the store runs along pixels.
+//
+// A short-K (128), narrow-N GEMM over ~1M pixels: the implicit-GEMM conv ran it at 40 TFLOP/s
+// (4 k-tiles per block, its prologue / epilogue dominating). Here a tile = 64 consecutive pixels
+// of one image x all N output channels (NT 16-channel tiles): the 64 pixel rows (all K channels,
+// one contiguous NHWC run each) are staged in LDS beside the block's weights, then each wave
+// runs its 16 pixels x NT tiles over the whole K on v_mfma_f32_16x16x4_f32 with channels as the
+// MFMA rows and pixels as its columns, so a lane group's 16 results of one channel are 16
+// consecutive pixels: the NCHW store is a 64-B run per channel. One ds_read_b128 of a pixel's
+// (or a weight row's) 4 k-values feeds 4 MFMAs (k = 4g + s over the 4 lane groups).
+#include "krrn_common.h"
+
+namespace {
+
+constexpr int kPx = 64;  // pixels per block (16 per wave)
+
+// Persistent blocks: the weights are staged once per block, then the block walks its 64-pixel
+// tiles (b, px0), the next tile's pixel rows loaded into registers while the current tile's
+// MFMAs run (8 float4 per thread), written to LDS after the barrier.
+template <int NT>
+__global__ __launch_bounds__(256) void conv1x1_nchw_kernel(const float* __restrict__ in, int in_cs, int in_co, int B,
+                                                           int HW, int K, int Kp, const float* __restrict__ wt, int N,
+                                                           int n_store, const float* __restrict__ scale,
+                                                           const float* __restrict__ bias, float* __restrict__ out,
+                                                           int out_cs, int out_co) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int pitch = Kp + 4;  // odd number of 16-B slots per row: conflict-free b128 reads
+  float* sx = lds;                  // [kPx][pitch]
+  float* sw = lds + kPx * pitch;    // [16 NT][pitch]
+  const int tid = threadIdx.x;
+  const int kq = Kp / 4;
+  const int tpi = krrn_cdiv(HW, kPx), ntiles = B * tpi;
+  for (int e = tid; e < 16 * NT * kq; e += 256) {
+    const int n = e / kq, q = e - (e / kq) * kq;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (n < N && 4 * q < K) v = *reinterpret_cast<const f32x4*>(wt + (long long)n * K + 4 * q);
+    *reinterpret_cast<f32x4*>(sw + n * pitch + 4 * q) = v;
+  }
+  // this thread's staging elements: e = tid + 256 u over kPx * kq (<= 64 * 64 / 256 = 16 float4)
+  constexpr int kMaxU = 16;
+  const int nu = krrn_cdiv(kPx * kq, 256);
+  auto load_x = [&](int tile, f32x4 (&r)[kMaxU]) {
+    const int b = tile / tpi, px0 = (tile - b * tpi) * kPx;
+    const float* xb = in + ((long long)b * HW) * in_cs + in_co;
+#pragma unroll
+    for (int u = 0; u < kMaxU; ++u) {
+      r[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int e = tid + 256 * u;
+      if (u < nu && e < kPx * kq) {
+        const int p = e / kq, q = e - (e / kq) * kq;
+        if (px0 + p < HW && 4 * q < K) r[u] = *reinterpret_cast<const f32x4*>(xb + (long long)(px0 + p) * in_cs + 4 * q);
+      }
+    }
+  };
+  const int lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const float* xr = sx + (16 * wave + fr) * pitch + 4 * g;  // this lane's pixel, k-quad g
+  const float* wr = sw + fr * pitch + 4 * g;                 // channel fr of tile t at + t * 16 * pitch
+  f32x4 xn[kMaxU];
+  if (blockIdx.x < ntiles) load_x(blockIdx.x, xn);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's MFMAs are done reading sx (and sw is staged)
+#pragma unroll
+    for (int u = 0; u < kMaxU; ++u) {
+      const int e = tid + 256 * u;
+      if (u < nu && e < kPx * kq) {
+        const int p = e / kq, q = e - (e / kq) * kq;
+        *reinterpret_cast<f32x4*>(sx + p * pitch + 4 * q) = xn[u];
+      }
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) load_x(tile + gridDim.x, xn);  // in flight under the MFMAs
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < Kp; k0 += 16) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + k0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(wr + t * 16 * pitch + k0);
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[s2], xv[s2], acc[t], 0, 0, 0);
+      }
+    }
+    // acc[t][i] = (channel 16 t + 4 g + i, pixel 16 wave + fr)
+    const int b = tile / tpi, px = (tile - b * tpi) * kPx + 16 * wave + fr;
+    if (px < HW) {
+      float* ob = out + ((long long)b * out_cs + out_co) * HW + px;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = 16 * t + 4 * g + i;
+          if (n < n_store) ob[(long long)n * HW] = acc[t][i] * (scale ? scale[n] : 1.f) + (bias ? bias[n] : 0.f);
+        }
+    }
+  }
+}
+
+}  // namespace
+
+KRRN_API int krrn_conv1x1_nchw_f32(const float* in, int in_cs, int in_co, int B, int HW, int cin, const float* wt,
+                                   int N, int n_store, const float* scale, const float* bias, float* out, int out_cs,
+                                   int out_co, void* stream) {
+  if (!in || !wt || !out) return KRRN_EARG;
+  if (B < 1 || HW < 1 || cin < 4 || N < 1 || N > 80 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
+  if ((cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(in) || !krrn_aligned16(wt)) return KRRN_EALIGN;
+  if (out_co + n_store > out_cs || (long long)B * HW * in_cs >= (1LL << 40)) return KRRN_ESHAPE;
+  if (cin > 256 || (long long)B * krrn_cdiv(HW, kPx) > 0x7fffffffLL) return KRRN_ESHAPE;  // kMaxU float4 per thread
+  const int Kp = (cin + 15) / 16 * 16;
+  const int nt = (N + 15) / 16;
+  const size_t lds = sizeof(float) * (size_t)(kPx + 16 * nt) * (Kp + 4);
+  if (lds > 160 * 1024) return KRRN_ESHAPE;
+  const int ntiles = B * krrn_cdiv(HW, kPx);
+  const int per_cu = (int)((160 * 1024) / lds);
+  const dim3 grid(min(ntiles, 256 * (per_cu < 1 ? 1 : per_cu)));
+  hipStream_t s = (hipStream_t)stream;
+#define KRRN_1X1(NTV)                                                                                                   \
+  if (nt == NTV) {                                                                                                      \
+    if (lds > 64 * 1024) {                                                                                              \
+      const hipError_t e = hipFuncSetAttribute((const void*)conv1x1_nchw_kernel<NTV>,                                  \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                  \
+      if (e != hipSuccess) return (int)e;                                                                               \
+    }                                                                                                                   \
+    hipLaunchKernelGGL(conv1x1_nchw_kernel<NTV>, grid, dim3(256), lds, s, in, in_cs, in_co, B, HW, cin, Kp, wt, N,     \
+                       n_store, scale, bias, out, out_cs, out_co);                                                      \
+    return krrn_launch_status();                                                                                        \
+  }
+  KRRN_1X1(1) KRRN_1X1(2) KRRN_1X1(3) KRRN_1X1(4) KRRN_1X1(5)
+#undef KRRN_1X1
+  return KRRN_ESHAPE;
+}

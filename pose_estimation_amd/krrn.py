@@ -187,7 +187,17 @@ class KRRNPlan:
         self.nbytes = plan_bytes(plan) + plan_bytes(getattr(self, "device_perm_plan", None))
 
     def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):
+        """The heads' final 1x1 conv + bias written NCHW (krrn.py:97-98, 80-84):
+        krrn_conv1x1_nchw_f32 (the implicit-GEMM conv's NCHW epilogue beyond its limits)."""
         B, Cx, Ho, Wo = out.shape
+        np_ = pad4(spec.cout)
+        if len(spec.taps[0]) == 1 and spec.stride == 1 and spec.cin_p <= 256 and np_ <= 80:
+            self.plan.add("krrn_conv1x1_nchw_f32", ptr(x.t), x.cs, x.co, x.B, Ho * Wo, spec.cin_p, ptr(spec.wt[0]), np_,
+                          n_store, ptr(spec.scale), ptr(spec.bias), ptr(out), Cx, 0,
+                          meta=dict(kernel="conv1x1_nchw", flops=2.0 * spec.cin * n_store * B * Ho * Wo,
+                                    tag="head_final", M=B * Ho * Wo, N=np_, K=spec.cin_p, splits=1,
+                                    mfma_flops=2.0 * spec.cin_p * 16 * ((np_ + 15) // 16) * B * Ho * Wo))
+            return
         add_conv(self.plan, x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=Ho, Wg=Wo,
                  in_s=spec.stride, taps=spec.taps[0], wt=ptr(spec.wt[0]), N=pad4(spec.cout), n_store=n_store,
                  scale=ptr(spec.scale), bias=ptr(spec.bias), out=ptr(out), out_cs=Cx, out_co=0, Ho=Ho, Wo=Wo,

@@ -304,3 +304,31 @@ def test_conv_small_group(dev):
         for outs, *_ in singles:
             assert not torch.isnan(outs[0]).any()
             assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("B,HW,cin,cout,co,oc,Cx", [(3, 1000, 128, 72, 0, 0, 72), (2, 777, 128, 3, 0, 0, 3),
+                                                   (4, 64, 20, 40, 4, 5, 50), (1, 130, 256, 80, 0, 0, 80)])
+def test_conv1x1_nchw(dev, B, HW, cin, cout, co, oc, Cx):
+    """krrn_conv1x1_nchw_f32 (the heads' final 1x1 convs) vs torch fp32: ragged pixel tiles, K not a
+    multiple of 16, channel-offset input and output."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, ptr
+    g = torch.Generator().manual_seed(HW + cin + cout)
+    W = HW // 2 if HW % 2 == 0 else HW
+    H = HW // W
+    conv = nn.Conv2d(cin, cout, 1, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
+        conv.bias.copy_(torch.randn(cout, generator=g))
+    x = torch.randn(B, cin, H, W, generator=g)
+    ref = conv(x).detach()
+    xa = _nhwc(x, dev, cs=ops.pad4(cin) + co + 4, co=co)
+    spec = ops.make_conv(conv, None, dev, cin_p=ops.pad4(cin))
+    out = torch.full((B, Cx, H, W), float("nan"), device=dev)
+    _lib.check(_lib.lib().krrn_conv1x1_nchw_f32(ptr(xa.t), xa.cs, xa.co, B, HW, ops.pad4(cin), ptr(spec.wt[0]),
+                                                ops.pad4(cout), cout, ptr(spec.scale), ptr(spec.bias), ptr(out), Cx, oc,
+                                                P(torch.cuda.current_stream().cuda_stream)), "conv1x1 nchw")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out[:, oc:oc + cout].cpu(), ref, **TOL)
+    if oc:
+        assert torch.isnan(out[:, :oc]).all()
