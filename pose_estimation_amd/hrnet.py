@@ -29,7 +29,7 @@ import torch.nn as nn
 from . import ops
 from .config import load_hrnet_spec
 from .ops import Act, pad4
-from .runtime import add_conv_group, add_small_group, Plan, add_conv, ptr
+from .runtime import add_conv_group, add_gemm, add_small_group, Plan, add_conv, ptr
 
 # HRNet branch convs as per-branch chains on plan streams (KRRN_HR_GROUP=0) or as grouped
 # launches, one per block depth (KRRN_HR_GROUP=1)
@@ -41,6 +41,8 @@ CONVT_GROUP = os.environ.get("KRRN_CONVT_GROUP", "1") == "1"
 CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
 # narrow 3x3 stride-1 convs (the HRNet branches' BasicBlocks) on the LDS-staged direct kernel
 SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
+# wide 1x1 convs as hipBLASLt GEMMs
+GEMM_1X1 = os.environ.get("KRRN_GEMM_1X1", "1") == "1"
 
 BN_MOMENTUM = 0.1
 
@@ -225,9 +227,22 @@ class _Builder:
             self.emit_wino(x, spec, U, out, res, relu)
         elif SMALL_CONV and ops.small_conv_eligible(spec, x):
             self.emit_small(x, spec, out, res, relu)
-        else:
+        elif not (GEMM_1X1 and self.emit_gemm(x, spec, out, res, relu)):
             self.emit_conv(x, spec, out, res, relu)
         return out
+
+    def emit_gemm(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool) -> bool:
+        """A wide 1x1 / stride-1 conv (layer1's Bottleneck projections, myhrnet.py:66-103) is a plain
+        GEMM over the NHWC rows: hipBLASLt through add_gemm (BN folded, residual + ReLU epilogue).
+        False (nothing emitted) when the layout or hipBLASLt does not fit."""
+        if not (spec.kind == "conv" and spec.ksize == 1 and spec.stride == 1 and out.co == 0
+                and (res is None or res.co == 0)):
+            return False
+        np_ = pad4(spec.cout)
+        return add_gemm(self.plan, a=x.t, a_off=x.co, lda=x.cs, M=x.B * x.H * x.W, wt=spec.wt[0], K=spec.cin_p,
+                        N=np_, scale=spec.scale, bias=spec.bias, out=out.t, ldo=out.cs, relu=relu,
+                        res=res.t if res is not None else None, ldr=res.cs if res is not None else 0,
+                        cin=spec.cin, cout=spec.cout, tag="conv1x1_gemm")
 
     @staticmethod
     def small_problem(x: Act, spec, out: Act, res: Optional[Act], relu: bool) -> dict:
