@@ -110,7 +110,7 @@ def _bn1d(bn: nn.BatchNorm1d, device):
 
 
 def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.Tensor, perms: Dict[str, torch.Tensor],
-                      hooks: Optional[Dict[str, List[Callable[[dict], None]]]] = None):
+                      hooks: Optional[Dict[str, List[Callable[[dict], None]]]] = None, materialize: bool = True):
     """Emit FusionNetLite.forward for P9 = [cloud | xyz_emb | nml_emb] ([B, N, 9] f32).
 
     perms: int32 device buffers 'v', 'x', 'n' ([N1] each, permutations of N), 'p1' ([N1]),
@@ -118,7 +118,8 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     hooks: optional callables run at named points of the emission ('level1' = after the level-1
     branch join, 'level2' = after the level-2 kNN), each given the level buffers complete at that
     point (feat1, feat2), e.g. to fork independent work onto a side stream where the fusion
-    leaves the chip underused.
+    leaves the chip underused. materialize=False skips writing the 1280-wide concat (returns None
+    for it): its only consumer, TBase conv1, reads the level rows by linearity.
     """
     hooks = hooks or {}
     dev = plan.device
@@ -151,7 +152,7 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     fm5 = plan.buf((B, N2, 512))
     nn1 = plan.buf((B, N), i32)
     nn2 = plan.buf((B, N), i32)
-    feat = plan.buf((B, N, 1280))
+    feat = plan.buf((B, N, 1280)) if materialize else None
 
     def knn(q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, out):
         plan.add("krrn_knn_f32", q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, B, ptr(out))
@@ -238,14 +239,15 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     # (posenet.build_tbase_plan), so the materialised concat (the module's output, kept for
     # inspection) is written on side stream FEAT_SID, off the critical path; the caller joins it.
     plan.join([3])
-    plan.fork([FEAT_SID])
-    with plan.on_stream(FEAT_SID):
-        plan.add("krrn_gather_rows_f32", ptr(nn2), 0, N, N, off(fm5, 0), N2 * 512, 512, off(feat, 0), N * 1280, 1280,
-                 512, B)
-        plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat1, 0), N * 384, 384, off(feat, 512), N * 1280,
-                 1280, 384, B)
-        plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat2, 0), N1 * 384, 384, off(feat, 896), N * 1280,
-                 1280, 384, B)
+    if materialize:
+        plan.fork([FEAT_SID])
+        with plan.on_stream(FEAT_SID):
+            plan.add("krrn_gather_rows_f32", ptr(nn2), 0, N, N, off(fm5, 0), N2 * 512, 512, off(feat, 0), N * 1280,
+                     1280, 512, B)
+            plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat1, 0), N * 384, 384, off(feat, 512),
+                     N * 1280, 1280, 384, B)
+            plan.add("krrn_gather_rows_f32", ptr(nn1), 0, N, N, off(feat2, 0), N1 * 384, 384, off(feat, 896),
+                     N * 1280, 1280, 384, B)
     plan.buffers.append(keep)
     return feat, dict(pool_v=nb4["v"], pool_x=nb4["x"], pool_n=nb4["n"], pool2=nb4b, idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1, nn2=nn2, feat1=feat1, feat2=feat2, fm5=fm5,
                       F0=F0, V1=V1, PV1=PV1, PV2=PV2, FP1=FP1, FP2=FP2, fm4=fm4)

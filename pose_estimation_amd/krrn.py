@@ -170,7 +170,8 @@ class KRRNPlan:
             if TBASE_EARLY:
                 hooks["level1"].append(tracked(emit_tb_l1))
             f0 = len(plan.ops)
-            feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms, hooks=hooks)
+            feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms, hooks=hooks,
+                                                       materialize=model.keep_fusion_feat)
             # the FusionNetLite launches (for the bench's fusion HBM roofline; hook ops excluded)
             self.fusion_op_ids = {id(op) for op in plan.ops[f0:] if id(op) not in side_ids and op.name != "sync"}
             self.feat = feat
@@ -180,7 +181,8 @@ class KRRNPlan:
             self.pred_t, self.tbase_bufs = build_tbase_plan(model.pose.t_net, plan, B, N, feat, "cls", "cloud",
                                                             cfg.Module.POSENet.INC_R, C, levels=levels,
                                                             pre=tb_pre or None, pre_sid=tb_sid)
-            plan.join([FEAT_SID])
+            if feat is not None:
+                plan.join([FEAT_SID])
         if pose_hook is not None:
             plan.join([psid])
         self.env = {"cls": self.cls, "cloud": self.cloud}
@@ -293,6 +295,9 @@ class KRRN(nn.Module):
         self._plans: "OrderedDict[Tuple, KRRNPlan]" = OrderedDict()
         self.plan_budget_bytes = PLAN_BUDGET
         self.return_views = False
+        # materialise FusionNetLite's 1280-wide output concat in the plan (plan.feat, for
+        # inspection / parity tests); TBase does not read it (conv1 by linearity on the level rows)
+        self.keep_fusion_feat = False
         self.perm_mode = "host"
 
     # plans fold the weights: any weight change invalidates them

@@ -1,5 +1,6 @@
 """Per-op serial device time of the HRNet backbone part of one plan (ops[:split]), with shapes,
-grouped by (kernel, tag, M, N, K); and the same for the heads (ops[split:heads_end]).
+grouped by (kernel, tag, M, N, K); and the same for the heads (ops[split:heads_end]) and the
+tail (fusion + TBase, ops[heads_end:]; the PnP pose plan is separate).
 usage (GPU box): python3 profiles/backbone_ops.py [B]"""
 import os
 import sys
@@ -25,7 +26,8 @@ st.load(make_batch(B, S, N, seed=1))
 st.run()
 torch.cuda.synchronize()
 kp = st.parts[0].kp
-for name, lo, hi in (("backbone", 0, kp.split), ("heads", kp.split, kp.heads_end)):
+for name, lo, hi in (("backbone", 0, kp.split), ("heads", kp.split, kp.heads_end),
+                     ("tail", kp.heads_end, len(kp.plan.ops))):
     sub = _sub_plan(kp.plan, lo, hi)
     sub.run_timed(dict(kp.env))
     prof = sub.run_timed(dict(kp.env))

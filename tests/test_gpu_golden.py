@@ -35,6 +35,7 @@ def test_krrn_golden(dev, name):
     m = KRRN(cfg=make_config(num_cls=C, backbone="w18"))
     init_weights(m, int(g["weight_seed"]))
     m = m.to(dev).eval()
+    m.keep_fusion_feat = True  # plan.feat is compared below
     t = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
     perms = [t(f"perm{i}") for i in range(5)]
     out = m(t("img"), t("cloud"), t("choose"), t("cls"), perms=perms)

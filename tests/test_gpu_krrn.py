@@ -135,6 +135,9 @@ def _check_parity(m, o, dev, B, S, N, d, crops=None, perms=None):
     """Run the HIP path on the whole batch `d` and the oracle on `crops` (all by default), both
     with the same pool permutations; returns the HIP outputs (cloned) for further checks."""
     torch.set_num_threads(8)
+    if not m.keep_fusion_feat:
+        m.keep_fusion_feat = True  # plan.feat is compared below
+        m.invalidate_plans()
     perms = _draw_perms(N, 11) if perms is None else perms
     out = m(d["img_croped"].to(dev), d["cloud"].to(dev), d["choose"].to(dev), d["cls_id"].to(dev),
             perms=[p.to(dev) for p in perms])
