@@ -6,6 +6,8 @@
 // (posenet.py:76-80 + krrn.py:153).
 #include <math.h>
 
+#include <cstdlib>
+
 #include "krrn_common.h"
 
 namespace {
@@ -62,6 +64,68 @@ __global__ void resize_bilinear_kernel(const float* __restrict__ in, int Hi, int
     r.x = fmaxf(r.x, 0.f); r.y = fmaxf(r.y, 0.f); r.z = fmaxf(r.z, 0.f); r.w = fmaxf(r.w, 0.f);
   }
   *reinterpret_cast<f32x4*>(out + opix * out_cs + out_co + 4 * c4) = r;
+}
+
+// Upsampling (Ho >= Hi, Wo >= Wi: adjacent outputs' source windows move by at most one pixel) as
+// 2x2 output pixels x one channel quad per thread: the four outputs read a 3x3 source patch (9
+// float4 loads instead of 16), each output combines its 2x2 of it with the same expression as
+// resize_bilinear_kernel (bit-identical results).
+__device__ __forceinline__ f32x4 pick3(const f32x4 (&r)[3], int i) { return i == 0 ? r[0] : (i == 1 ? r[1] : r[2]); }
+
+__global__ void resize_up2x2_kernel(const float* __restrict__ in, int Hi, int Wi, int in_cs, int in_co, int C4,
+                                    float* __restrict__ out, int Ho, int Wo, int out_cs, int out_co,
+                                    const float* __restrict__ add, int add_cs, int add_co, float sh, float sw,
+                                    int align, int relu, int Ho2, int Wo2, int total) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c4 = e % C4;
+  int p = e / C4;
+  const int ox2 = p % Wo2;
+  p /= Wo2;
+  const int oy2 = p % Ho2;
+  const int b = p / Ho2;
+  int y0[2], y1[2], x0[2], x1[2];
+  float ly0[2], ly1[2], lx0[2], lx1[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    src_index(min(2 * oy2 + d, Ho - 1), Hi, sh, align, y0[d], y1[d], ly0[d], ly1[d]);
+    src_index(min(2 * ox2 + d, Wo - 1), Wi, sw, align, x0[d], x1[d], lx0[d], lx1[d]);
+  }
+  const float* ib = in + (long long)b * Hi * Wi * in_cs + in_co + 4 * c4;
+  f32x4 P[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int yy = min(y0[0] + r, Hi - 1), xx = min(x0[0] + c, Wi - 1);
+      P[r][c] = *reinterpret_cast<const f32x4*>(ib + ((long long)yy * Wi + xx) * in_cs);
+    }
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy) {
+    const int oy = 2 * oy2 + dy;
+    if (oy >= Ho) break;
+    const int ra = y0[dy] - y0[0], rb = y1[dy] - y0[0];
+    f32x4 row0[3], row1[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      row0[c] = ra == 0 ? P[0][c] : P[1][c];
+      row1[c] = rb == 0 ? P[0][c] : (rb == 1 ? P[1][c] : P[2][c]);
+    }
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int ox = 2 * ox2 + dx;
+      if (ox >= Wo) break;
+      const int ca = x0[dx] - x0[0], cb = x1[dx] - x0[0];
+      const f32x4 v00 = pick3(row0, ca), v01 = pick3(row0, cb), v10 = pick3(row1, ca), v11 = pick3(row1, cb);
+      f32x4 r = ly0[dy] * (lx0[dx] * v00 + lx1[dx] * v01) + ly1[dy] * (lx0[dx] * v10 + lx1[dx] * v11);
+      const long long opix = ((long long)b * Ho + oy) * Wo + ox;
+      if (add) r = *reinterpret_cast<const f32x4*>(add + opix * add_cs + add_co + 4 * c4) + r;
+      if (relu) {
+        r.x = fmaxf(r.x, 0.f); r.y = fmaxf(r.y, 0.f); r.z = fmaxf(r.z, 0.f); r.w = fmaxf(r.w, 0.f);
+      }
+      *reinterpret_cast<f32x4*>(out + opix * out_cs + out_co + 4 * c4) = r;
+    }
+  }
 }
 
 template <typename IT>
@@ -274,6 +338,20 @@ KRRN_API int krrn_resize_bilinear_f32(const float* in, int B, int Hi, int Wi, in
   } else {
     sh = (float)Hi / (float)Ho;
     sw = (float)Wi / (float)Wo;
+  }
+  const int Ho2 = (Ho + 1) / 2, Wo2 = (Wo + 1) / 2;
+  const long long total2 = (long long)B * Ho2 * Wo2 * (C / 4);
+  // the 2x2 form for large upsamples only (the heads' 472 MB ones: 161 -> 118 us); the HRNet
+  // fuse layers' small ones want the 4x more threads of the plain kernel (7.6 vs 9.0 us)
+  static const long long up_min = [] {
+    const char* e = getenv("KRRN_RESIZE_UP_MIN");
+    return e ? atoll(e) : (1LL << 21);
+  }();
+  if (Ho >= Hi && Wo >= Wi && total2 >= up_min && total2 < 0x7fffffffLL) {
+    hipLaunchKernelGGL(resize_up2x2_kernel, grid1(total2), dim3(256), 0, (hipStream_t)stream, in, Hi, Wi, in_cs, in_co,
+                       C / 4, out, Ho, Wo, out_cs, out_co, add, add_cs, add_co, sh, sw, align_corners, relu, Ho2, Wo2,
+                       (int)total2);
+    return krrn_launch_status();
   }
   const long long total = (long long)B * Ho * Wo * (C / 4);
   if (total < 0x7fffffffLL)
