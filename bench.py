@@ -38,6 +38,7 @@ from pose_estimation_amd.synthetic import OBJ_DICT, init_weights, make_batch  # 
 
 METRIC = "crops/sec at 640×480 RGB-D, 1000 sampled pts; ADD(-S) AUC vs reference"
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
+PEAK_BF16_MFMA_TFLOPS = 2516.6  # MI355X_MICROARCH.md: dense bf16 MFMA, 1024 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
@@ -69,10 +70,11 @@ def roofline_from_profile(prof, B: int):
     groups = {}
     for op, ms in prof:
         k = op.meta.get("kernel", op.name)
-        g = groups.setdefault(k, {"ms": 0.0, "flops": 0.0, "mfma": 0.0, "n": 0})
+        g = groups.setdefault(k, {"ms": 0.0, "flops": 0.0, "mfma": 0.0, "bf16": 0.0, "n": 0})
         g["ms"] += ms
         g["flops"] += op.meta.get("flops", 0.0)
         g["mfma"] += op.meta.get("mfma_flops", op.meta.get("flops", 0.0))
+        g["bf16"] += op.meta.get("mfma_bf16_flops", 0.0)
         g["n"] += 1
     total_ms = sum(g["ms"] for g in groups.values())
     dom = max(groups, key=lambda k: groups[k]["ms"])
@@ -88,15 +90,18 @@ def roofline_from_profile(prof, B: int):
                  for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])}
     traffic, tsrc = _pmc_traffic(dom)
     # achieved = what the matrix pipe issues (for Winograd F(2x2,3x3) 2.25x fewer multiplies than the
-    # direct conv it replaces), so frac <= 1 is a roofline fraction; the direct-conv-equivalent
-    # rate (SURVEY §8d's FLOP formula) is kept as `effective_tflops`
-    mp = (g["mfma"] / g["n"]) / (avg_ms * 1e-3) / 1e12 if g["mfma"] > 0 else None
+    # direct conv it replaces; for the split-bf16 Winograd the 6 bf16 term products per f32 product,
+    # against the bf16 peak), so frac <= 1 is a roofline fraction; the direct-conv-equivalent rate
+    # (SURVEY §8d's FLOP formula) is kept as `effective_tflops`
+    bf16 = g["bf16"] > 0
+    pipe_fl, peak = (g["bf16"], PEAK_BF16_MFMA_TFLOPS) if bf16 else (g["mfma"], PEAK_F32_MFMA_TFLOPS)
+    mp = (pipe_fl / g["n"]) / (avg_ms * 1e-3) / 1e12 if pipe_fl > 0 else None
     roof = {"kernel": dom, "bound": "mfma", "achieved": round(mp, 2) if mp else None,
-            "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(mp / PEAK_F32_MFMA_TFLOPS, 4) if mp else None, "traffic": traffic,
+            "peak": peak, "unit": "TFLOP/s", "pipe": "bf16 (f32-accurate 3-term split)" if bf16 else "f32",
+            "frac": round(mp / peak, 4) if mp else None, "traffic": traffic,
             "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
             "launches": g["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
-            "mfma_flops_per_launch": round(g["mfma"] / g["n"]),
+            "mfma_flops_per_launch": round(pipe_fl / g["n"]),
             "effective_tflops": round(achieved, 2) if achieved else None,
             "effective_flops_per_launch": round(g["flops"] / g["n"]),
             "all_conv_gemm": {"ms_per_step": round(conv_ms, 3),
@@ -108,7 +113,8 @@ def roofline_from_profile(prof, B: int):
                          "mfma_pipe_frac": round(allc_mf / (allc_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)
                          if allc_ms else None,
                          "note": "every conv / GEMM of the step incl. Winograd; effective = direct-conv FLOPs "
-                                 "(SURVEY §8d), pipe = FLOPs the MFMA pipe issues"},
+                                 "(SURVEY §8d), pipe = FLOPs the MFMA pipe issues in f32-MFMA time (bf16 "
+                                 "FLOPs / 16)"},
             "events_ms_per_step": round(total_ms, 3)}
     return roof, breakdown
 

@@ -124,6 +124,16 @@ int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, i
  * 1 = ring-staged raw patches, transform beside the MFMAs; 2 = the same without that overlap;
  * 0 = the register-staged V image. All three give bit-identical results. */
 int krrn_wino_variant(int v);
+/* krrn_conv3x3_wino_f32 on the bf16 matrix cores at f32 accuracy: every operand split into
+ * three bf16 terms (x = x_h + x_m + x_l, round-to-nearest, exact), each product summed over the
+ * six term pairs hh, hm, mh, hl, lh, mm (the dropped ones are below 2^-23 |a b|), accumulated in
+ * f32. U3 is wino_weights' U split on the host (wino_weights_x3): plane U_mh
+ * [ceil(cin/8)][16][N][2][8] bf16 (m0..m3 h0..h3 of channels 4 half .. 4 half + 3) followed by
+ * plane U_l [ceil(cin/8)][16][N][2][4] bf16; U3 16-byte aligned. Other arguments as
+ * krrn_conv3x3_wino_f32. */
+int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* U3,
+                             int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
+                             int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
 
 /* Direct conv for narrow layers: 3x3 / pad 1 / stride 1 or 2, or 1x1 / stride 1 (the HRNet
  * branches' BasicBlock convs, lib/network/hrnet/myhrnet.py:34-63, and the fuse layers' stride-2

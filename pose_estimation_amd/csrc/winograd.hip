@@ -678,6 +678,204 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
   wino_epi_finish2d(a, smem, b, ty0, tx0, n0);
 }
 
+// ---- Split-bf16 ring kernel: the same block, ring and transform as wino_f23_ring_kernel<1>, the
+// 16 channel GEMMs on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16, 16x the f32 rate) at f32
+// accuracy. Every f32 operand is split round-to-nearest into three bf16 terms,
+// x = x_h + x_m + x_l with |x_m| <= 2^-8 |x|, |x_l| <= 2^-16 |x| (exact: 24 significand bits),
+// and a product a b is summed over the 6 term pairs h h, h m, m h, h l, l h, m m; the 3 dropped
+// (m l, l m, l l) are below 2^-23 |a b|, the size of the f32 MFMA's own product rounding, and
+// everything accumulates in f32 (profiles/bench_wino_x3.py: RMS error vs f64 2.8e-7 against the
+// f32 kernel's 3.0e-7).
+// Register chains, no copies but one: a lane's 8 bf16 of an MFMA operand are 2 term kinds x its 4
+// channels (k = 8 half + i pairs A and B element i of the same lane), so with the A chain
+// [V_h V_h V_m V_l] (4 x 2 registers) and the B chain [U_m U_h U_l] (one b128 of plane U_mh + one
+// b64 of plane U_l, 6 registers) the three MFMAs are
+//   A[0:3] x B[2:5] = hh + hl,   A[2:5] x B[0:3] = hm + mh,   A[4:7] x B[0:3] = mm + lh.
+// V is split in registers (v_cvt_pk_bf16_f32, RNE); U is split on the host (ops.wino_weights_x3).
+// Weight addresses: a per-lane voffset per n-block and the chunk / component part in soffset
+// (SALU); a wave reloads component v's weights for the next chunk as soon as its MFMAs have
+// issued (one weight buffer in registers: acc 128 + weights 48 VGPRs).
+// Measured (MI355X, profiles/bench_wino_x3.py, 64 x 128 -> 128): 120x120 1.03-1.06 ms against
+// the f32 ring kernel's 1.39-1.47 ms, 60x60 0.27 vs 0.37 ms; in the step 412 vs 483 us per launch
+// (12.99 vs 13.68 ms per step on one box). The bf16 MFMAs take ~280 us of the 1.05 ms: timing
+// experiments (KRRN_WINO_EXP) put the rest in VALU issue (the split is 5.5 VALU per value, the
+// transform ~2.5; a build with no MFMAs and no loads still takes 0.65 ms), then the weight and raw
+// loads (-15 % / -11 % without them) and the epilogue (-15 %). Rejected: a 64-tile, 512-thread
+// block (2 components x 2 tile-blocks x 2 n-blocks per wave: half the weight loads per MFMA and a
+// bank-conflict-free ring layout, but one block per CU: 1.05-1.12 ms), sched_barrier-pinned
+// reloads (no change).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));  // RNE
+}
+__device__ __forceinline__ float bf_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float bf_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xFFFF0000u); }
+
+// x (4 channels) -> the A chain [x_h x_h x_m x_l] as packed bf16 pairs
+__device__ __forceinline__ u32x8 split3_chain(const f32x4 x) {
+  const unsigned h0 = pk_bf16(x[0], x[1]), h1 = pk_bf16(x[2], x[3]);
+  const float r0 = x[0] - bf_lo(h0), r1 = x[1] - bf_hi(h0);
+  const float r2 = x[2] - bf_lo(h1), r3 = x[3] - bf_hi(h1);
+  const unsigned m0 = pk_bf16(r0, r1), m1 = pk_bf16(r2, r3);
+  const unsigned l0 = pk_bf16(r0 - bf_lo(m0), r1 - bf_hi(m0)), l1 = pk_bf16(r2 - bf_lo(m1), r3 - bf_hi(m1));
+  return u32x8{h0, h1, h0, h1, m0, m1, l0, l1};
+}
+
+__device__ __forceinline__ bf16x8 sub4(const u32x8& c, int o) {
+  return __builtin_bit_cast(bf16x8, u32x4{c[o], c[o + 1], c[o + 2], c[o + 3]});
+}
+
+__global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * 2 * kWT * kSP];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gxn = krrn_cdiv(a.Wt, kGX), gyn = krrn_cdiv(a.Ht, kGY), nbn = krrn_cdiv(a.N, kWN);
+  const int per_img = gxn * gyn;
+  const int bid = krrn_xcd_remap(blockIdx.x, a.B * per_img * nbn);
+  const int sp = bid / nbn, nb = bid - (bid / nbn) * nbn;
+  const int b = sp / per_img, r2 = sp - (sp / per_img) * per_img;
+  const int by = r2 / gxn, bx = r2 - (r2 / gxn) * gxn;
+  const int n0 = nb * kWN;
+  const int ty0 = by * kGY, tx0 = bx * kGX;
+  const int nck = krrn_cdiv(a.cin, kWC);
+
+  // raw staging: this thread's 2 pieces (pixel q/2 of the block's raw region, channel half q&1);
+  // the chunk's channel offset goes in soffset
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.in + (size_t)b * a.img + a.in_co), (short)0, (int)min(a.img * 4 - (long long)a.in_co * 4, 0x7FFFFFFFLL),
+      0x00020000);
+  unsigned roff[2], roffm[2];  // roffm: the upper channel half masked (a last chunk of 4 channels)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + 256 * i;
+    const int pix = q >> 1, hh = q & 1;
+    const int rr = pix / kRC, rc = pix - (pix / kRC) * kRC;
+    const int iy = 2 * ty0 - 1 + rr, ix = 2 * tx0 - 1 + rc;
+    const bool ok = q < kRPieces && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    roff[i] = ok ? (unsigned)((((long long)iy * a.W + ix) * a.in_cs + 4 * hh) * 4) : kWOOB;
+    roffm[i] = hh ? kWOOB : roff[i];
+  }
+  auto load_raw = [&](int ck, f32x4 (&r)[2]) {  // chunks past the last reload the last (unused)
+#if KRRN_WINO_EXP == 6  // timing experiment: the first chunk's raw input only
+    if (ck > 0) return;
+#endif
+    ck = min(ck, nck - 1);
+    const bool half = ck * kWC + 4 >= a.cin;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      r[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, half ? roffm[i] : roff[i],
+                                                                            ck * kWC * 4, 0));
+  };
+  auto store_raw = [&](int slot, const f32x4 (&r)[2]) {
+    float* dst = smem + slot * kRSlot;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dst + 4 * (tid + 256 * i)) = r[i];
+  };
+
+  // split weights, record (chunk, xi, n, half): 16 B of plane U_mh, 8 B of plane U_l. Lanes of n
+  // past N read channel N-1 (finite; those output columns are never stored).
+  const int fr = lane & 31, h = lane >> 5;
+  const long long nrec = (long long)nck * 16 * a.N * 2;
+  const char* u3 = reinterpret_cast<const char*>(a.U);
+  const __amdgpu_buffer_rsrc_t rsMH =
+      __builtin_amdgcn_make_buffer_rsrc((void*)u3, (short)0, (int)min(nrec * 16, 0x7FFFFFFFLL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsL =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(u3 + nrec * 16), (short)0, (int)min(nrec * 8, 0x7FFFFFFFLL), 0x00020000);
+  unsigned wrec[kNJ];  // per-lane record part: 2 n + half
+#pragma unroll
+  for (int j = 0; j < kNJ; ++j) wrec[j] = (unsigned)(2 * min(n0 + 32 * j + fr, a.N - 1) + h);
+  u32x4 wmh[4][kNJ];
+  u32x2 wl[4][kNJ];
+  auto load_wv = [&](int ck, int v) {
+#if KRRN_WINO_EXP == 5  // timing experiment: the first chunk's weights only
+    if (ck > 0) return;
+#endif
+    ck = min(ck, nck - 1);
+    const unsigned srec = (unsigned)(((ck * 16 + 4 * wave + v) * a.N) * 2);  // uniform
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) {
+      wmh[v][j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsMH, wrec[j] * 16u, srec * 16u, 0));
+      wl[v][j] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsL, wrec[j] * 8u, srec * 8u, 0));
+    }
+  };
+
+  // this lane's patch rows: t_u = d[ra] +- d[rb] (B^T row u = wave)
+  const int ra = wave == 0 ? 0 : (wave == 2 ? 2 : 1);
+  const int rb = wave == 0 ? 2 : (wave == 3 ? 3 : (wave == 1 ? 2 : 1));
+  const int tx = fr % kGX, ty = fr / kGX;
+  const int pa = ((2 * ty + ra) * kRC + 2 * tx) * 2 + h;
+  const int pb = ((2 * ty + rb) * kRC + 2 * tx) * 2 + h;
+
+  f32x16 acc[4][kNJ];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
+
+  // scalar f32 arithmetic (built without SLP packing: v_pk_*_f32 beside MFMAs costs extra issue)
+  const float sgn = wave == 1 ? 1.f : -1.f;
+  auto make_v = [&](const float* sl, f32x4 (&V)[4]) {
+    f32x4 t[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 da = *reinterpret_cast<const f32x4*>(sl + 4 * (pa + 2 * c));
+      const f32x4 db = *reinterpret_cast<const f32x4*>(sl + 4 * (pb + 2 * c));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[c][e] = __builtin_fmaf(sgn, db[e], da[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      V[0][e] = t[0][e] - t[2][e];
+      V[1][e] = t[1][e] + t[2][e];
+      V[2][e] = t[2][e] - t[1][e];
+      V[3][e] = t[1][e] - t[3][e];
+    }
+  };
+
+  f32x4 raw[2];
+  load_raw(0, raw);
+#pragma unroll
+  for (int v = 0; v < 4; ++v) load_wv(0, v);
+  store_raw(0, raw);
+  load_raw(1, raw);
+  __syncthreads();
+  store_raw(1, raw);
+  load_raw(2, raw);
+  __syncthreads();
+  for (int ck = 0; ck < nck; ++ck) {
+    f32x4 V[4];
+    make_v(smem + (ck % 3) * kRSlot, V);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const u32x8 ac = split3_chain(V[v]);
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j) {
+        const u32x8 bc = {wmh[v][j][0], wmh[v][j][1], wmh[v][j][2], wmh[v][j][3], wl[v][j][0], wl[v][j][1], 0u, 0u};
+        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 2), acc[v][j], 0, 0, 0);
+        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 2), sub4(bc, 0), acc[v][j], 0, 0, 0);
+        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 4), sub4(bc, 0), acc[v][j], 0, 0, 0);
+      }
+      load_wv(ck + 1, v);
+      // keep the reload here (hipcc otherwise sinks every weight load below all the MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    store_raw((ck + 2) % 3, raw);
+    load_raw(ck + 3, raw);
+    __syncthreads();
+  }
+  wino_epi_put(smem, acc);
+  __syncthreads();
+  wino_epi_finish2d(a, smem, b, ty0, tx0, n0);
+}
+
 }  // namespace
 
 // kernel choice (krrn_wino_variant): 1 = the ring kernel with the next chunk's transform beside
@@ -731,5 +929,37 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
     else
       hipLaunchKernelGGL(wino_f23_ring_kernel<1>, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
   }
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
+                                      const void* U3, int N, int n_store, const float* scale, const float* bias,
+                                      const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
+                                      int relu, void* stream) {
+  if (!in || !U3 || !out) return KRRN_EARG;
+  if (B < 1 || H < 1 || W < 1 || N < 1 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
+  if (cin < 4 || (cin & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(U3) || (((uintptr_t)in) & 3u)) return KRRN_EALIGN;
+  if (out_co + n_store > out_cs) return KRRN_ESHAPE;
+  WinoArgs a;
+  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = H; a.W = W; a.cin = cin;
+  a.img = (long long)H * W * in_cs;
+  a.U = reinterpret_cast<const float*>(U3); a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
+  a.res = res; a.res_cs = res_cs; a.res_co = res_co;
+  a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.relu = relu;
+  a.Ht = (H + 1) / 2; a.Wt = (W + 1) / 2;
+  const bool ov = !(out_cs & 3) && !(out_co & 3) && krrn_aligned16(out);
+  const bool rv = !res || (!(res_cs & 3) && !(res_co & 3) && krrn_aligned16(res));
+  const bool sv = (!scale || krrn_aligned16(scale)) && (!bias || krrn_aligned16(bias));
+  a.vec = (ov && rv && sv && !(n_store & 3)) ? 1 : 0;
+  const long long T = (long long)B * a.Ht * a.Wt;
+  if (T > 0x7fffffffLL) return KRRN_ESHAPE;
+  a.T = (int)T;
+  // 32-bit buffer offsets: one image, and the U_hm plane (records x 16 B)
+  const long long nrec = (long long)krrn_cdiv(cin, kWC) * 16 * N * 2;
+  if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
+  const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kWN);
+  if (rb > 0x7fffffffLL) return KRRN_ESHAPE;
+  hipLaunchKernelGGL(wino_f23_x3_kernel, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }

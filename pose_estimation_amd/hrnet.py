@@ -43,6 +43,8 @@ CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
 SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
 # wide 1x1 convs as hipBLASLt GEMMs
 GEMM_1X1 = os.environ.get("KRRN_GEMM_1X1", "1") == "1"
+# Winograd convs on the bf16 matrix cores with f32-accurate split operands (krrn_conv3x3_wino_x3_f32)
+WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
 
 BN_MOMENTUM = 0.1
 
@@ -223,6 +225,8 @@ class _Builder:
         assert (out.H, out.W) == (Ho, Wo) and out.cp >= pad4(spec.cout)
         if ops.wino_eligible(spec, x.B * Ho * Wo) and x.cs % 2 == 0 and x.co % 2 == 0:
             U = ops.wino_weights(conv, self.dev, cin_map=cin_map, cin_p=x.cp)
+            if WINO_X3:
+                U = ops.wino_weights_x3(U)
             self.specs.append(U)
             self.emit_wino(x, spec, U, out, res, relu)
         elif SMALL_CONV and ops.small_conv_eligible(spec, x):
@@ -270,15 +274,24 @@ class _Builder:
 
     def emit_wino(self, x: Act, spec, U: torch.Tensor, out: Act, res: Optional[Act], relu: bool,
                   tag: str = "conv"):
+        """Fused Winograd F(2x2,3x3): on the bf16 matrix cores with split operands (U = the
+        wino_weights_x3 planes) or on the f32 ones (U f32)."""
         np_ = pad4(spec.cout)
         M = x.B * out.H * out.W
-        self.plan.add("krrn_conv3x3_wino_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(U), np_, np_,
-                      ptr(spec.scale), ptr(spec.bias), ptr(res.t) if res is not None else ptr(None),
-                      res.cs if res is not None else 0, res.co if res is not None else 0, ptr(out.t), out.cs,
-                      out.co, int(relu),
-                      meta=dict(kernel="wino_f23<32,32,16>", flops=2.0 * spec.cin * spec.cout * 9 * M, tag=tag + "_wino",
-                                M=M, N=np_, K=spec.cin_p * 9,
-                                mfma_flops=2.0 * 16 * spec.cin_p * np_ * x.B * ((out.H + 1) // 2) * ((out.W + 1) // 2)))
+        x3 = U.dtype == torch.bfloat16
+        tiles = x.B * ((out.H + 1) // 2) * ((out.W + 1) // 2)
+        # matrix-pipe FLOPs: f32 MFMA 2 per (component, tile, channel in, channel out); the split
+        # kernel issues 6 bf16 term products each (12 FLOPs) at 16x the f32 rate, counted here in
+        # f32-pipe time (/ 16) so all_conv's pipe fraction stays one scale
+        pipe = 2.0 * 16 * spec.cin_p * np_ * tiles
+        meta = dict(kernel="wino_f23_x3" if x3 else "wino_f23<32,32,16>", flops=2.0 * spec.cin * spec.cout * 9 * M,
+                    tag=tag + "_wino", M=M, N=np_, K=spec.cin_p * 9, mfma_flops=pipe * 6 / 16 if x3 else pipe)
+        if x3:
+            meta["mfma_bf16_flops"] = pipe * 6
+        self.plan.add("krrn_conv3x3_wino_x3_f32" if x3 else "krrn_conv3x3_wino_f32", ptr(x.t), x.cs, x.co, x.B, x.H,
+                      x.W, spec.cin_p, ptr(U), np_, np_, ptr(spec.scale), ptr(spec.bias),
+                      ptr(res.t) if res is not None else ptr(None), res.cs if res is not None else 0,
+                      res.co if res is not None else 0, ptr(out.t), out.cs, out.co, int(relu), meta=meta)
 
     def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         np_ = pad4(spec.cout)

@@ -227,6 +227,28 @@ def wino_weights(conv: torch.nn.Conv2d, device, cin_map: Optional[List[int]] = N
     return out.float().contiguous().to(device)
 
 
+def split_bf16x3(u: torch.Tensor):
+    """f32 -> three bf16 terms, each the round-to-nearest of what the previous ones left:
+    u = h + m + l exactly (24 significand bits), |m| <= 2^-8 |u|, |l| <= 2^-16 |u|."""
+    u = u.float()
+    h = u.bfloat16()
+    r = u - h.float()
+    m = r.bfloat16()
+    l = (r - m.float()).bfloat16()
+    return h, m, l
+
+
+def wino_weights_x3(U: torch.Tensor) -> torch.Tensor:
+    """wino_weights' U [nck][16][N][8] f32 -> the split planes krrn_conv3x3_wino_x3_f32 reads, as
+    one bf16 tensor: U_mh [nck][16][N][half][m0..m3 h0..h3] then U_l [nck][16][N][half][l0..l3]
+    (half = channels 4 half .. 4 half + 3 of the chunk)."""
+    h, m, l = split_bf16x3(U)
+    nck, _, N, _ = U.shape
+    h, m, l = (t.reshape(nck, 16, N, 2, 4) for t in (h, m, l))
+    mh = torch.cat([m, h], dim=-1).reshape(-1)
+    return torch.cat([mh, l.reshape(-1)]).contiguous()
+
+
 def wino_eligible(spec: ConvSpec, M: int) -> bool:
     """Fused Winograd for the wide stride-1 3x3 convs (>= 32 channels in and out, >= 32k output
     pixels); the narrow HRNet branches stay on the implicit GEMM (latency-bound there)."""

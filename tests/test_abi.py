@@ -8,7 +8,7 @@ import re
 import pytest
 
 from pose_estimation_amd import _lib
-from pose_estimation_amd import runtime  # noqa: F401  (registers the signatures)
+from pose_estimation_amd import bpnp, dataset, fps, loss, metric, runtime  # noqa: F401  (register the signatures)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "krrn_hip.h")

@@ -222,6 +222,20 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     assert torch.count_nonzero(outs[0][..., np_:]).item() == 0
     # the three kernels are bit-identical (same V operands and MFMA order), every output written
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    # the split-bf16 kernel: f32 accuracy (the f32 kernel's tolerance against torch, and within
+    # f32 accumulation noise of the f32 kernel), every output written, pad channels zero
+    U3 = ops.wino_weights_x3(U)
+    out.t.fill_(float("nan"))
+    out.t[..., np_:] = 0.0
+    _lib.check(L.krrn_conv3x3_wino_x3_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_, np_,
+                                          ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t), out.cs, 0,
+                                          1, P(torch.cuda.current_stream().cuda_stream)), "wino_x3")
+    torch.cuda.synchronize()
+    got3 = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got3, ref, **TOL)
+    assert torch.count_nonzero(out.t[..., np_:]).item() == 0
+    scale = float(ref.abs().max())
+    torch.testing.assert_close(got3, got, rtol=1e-5, atol=2e-6 * scale)
 
 
 @pytest.mark.parametrize("B,cin,cout,H,W,co,nw,ks,k,st", [
