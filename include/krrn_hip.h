@@ -80,12 +80,25 @@ typedef struct krrn_conv_desc {
   float* workspace;
 } krrn_conv_desc;
 
-/* Up to 4 independent convolutions in ONE launch with a shared tile shape (tile 6 = 128x32x32
- * or 8 = 64x64x32), each with its own split-K factor: the j-th conv of every HRNet branch of a
+/* Up to 4 independent convolutions in ONE launch with a shared tile shape (tile 1 = 128x128x16,
+ * 6 = 128x32x32 or 8 = 64x64x32), each with its own split-K factor: the j-th conv of every HRNet branch of a
  * HighResolutionModule (myhrnet.py:177-225: branch i is a chain of BasicBlocks on its own
  * resolution, so the branches are independent until the fuse layer). Each problem computes
  * exactly what krrn_conv2d_f32 would with the same descriptor. */
 int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* stream);
+
+/* krrn_conv2d_f32 / krrn_conv2d_group_f32 on the bf16 matrix cores at f32 accuracy (NHWC output,
+ * every tile of the menu / tiles 1, 6, 8): the activations are split while staged, the weights beforehand, into
+ * three bf16 terms each (x = x_h + x_m + x_l, round-to-nearest, exact); every product is summed
+ * over the six term pairs hh, hm, mh, hl, lh, mm (the dropped ones are below 2^-23 |a b|) and
+ * accumulated in f32. wt3 (or each desc's wt) holds the split weights, bf16 [N][K / 4][16]: per 4 k
+ * the terms m0..m3 h0..h3 l0..l3 then 4 zeros (ops.conv_weights_x3); 16-byte aligned. */
+int krrn_conv2d_x3_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin, int Hg, int Wg,
+                       int in_s, int ntaps, const int* tap_dy, const int* tap_dx, const void* wt3, int N, int n_store,
+                       const float* scale, const float* bias, const float* bias2, int b2_div, const float* res,
+                       int res_cs, int res_co, float* out, int out_cs, int out_co, int Ho, int Wo, int osy, int osx,
+                       int ooy, int oox, int relu, int tile, int splits, float* workspace, void* stream);
+int krrn_conv2d_group_x3_f32(const krrn_conv_desc* descs, int n, int tile, void* stream);
 
 /* Plain f32 GEMM on hipBLASLt (library-shaped GEMMs of the fusion / TBase, see blas.hip):
  *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n*K + k] + bias[n] + res[m*ldr + n]),  0 <= n < N

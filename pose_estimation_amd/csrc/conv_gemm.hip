@@ -83,23 +83,62 @@ struct Cfg {
   static constexpr int PITCH = BK + 4;          // odd number of 16-B slots
   static constexpr bool A_FULL = AL * RPP == BM, B_FULL = BL * RPP == BN;  // no partial staging pass
   static constexpr int A_FLOATS = BM * PITCH, B_FLOATS = BN * PITCH;
+  // split-bf16 operands (X3): 32 B per 4 k (a bf16 chain) per row, row pitch 2 BK + 4 dwords (an
+  // odd number of 16-B slots)
+  static constexpr int PX = 2 * BK + 4;
+  static constexpr int A_X3 = BM * PX, B_X3 = BN * PX;
+  static constexpr int BLOCKS_X3 = 2 * (A_X3 + B_X3) * 4 > 80 * 1024 ? 1 : 2;  // blocks per CU by LDS
   static_assert(MI >= 1 && NI >= 1, "wave tile must be at least 32x32");
   static_assert(BK % 8 == 0, "BK multiple of 8");
 };
 
-template <int AL, int BL>
+// ---- split-bf16 operands (X3) ------------------------------------------------------------------
+// f32 operands split round-to-nearest into three bf16 terms x = x_h + x_m + x_l (exact, 24
+// significand bits); a product is summed over the term pairs hh, hm, mh, hl, lh, mm (the dropped
+// ml, lm, ll are below 2^-23 |a b|, the f32 product rounding), accumulated in f32 on
+// v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate: 2.67x per f32 product). A lane's 8 bf16 of an
+// MFMA operand are 2 term kinds x its 4 k (element i of A pairs with element i of B): the
+// activations are split once while staged, into the LDS chain [h h m l] per 4 k, the weights on
+// the host into [m h l 0] (ops.conv_weights_x3), so the three MFMAs per 8 k read register slices:
+//   A[0:3] x B[2:5] = hh + hl,   A[2:5] x B[0:3] = hm + mh,   A[4:7] x B[0:3] = mm + lh.
+typedef __bf16 cg_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 cg_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float cg_f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned cg_u32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned cg_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned cg_pk(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(cg_f32x2{a, b}, cg_bf16x2));  // RNE
+}
+
+__device__ __forceinline__ cg_u32x8 cg_split_chain(const f32x4 x) {
+  const unsigned h0 = cg_pk(x[0], x[1]), h1 = cg_pk(x[2], x[3]);
+  const float r0 = x[0] - __builtin_bit_cast(float, h0 << 16), r1 = x[1] - __builtin_bit_cast(float, h0 & 0xFFFF0000u);
+  const float r2 = x[2] - __builtin_bit_cast(float, h1 << 16), r3 = x[3] - __builtin_bit_cast(float, h1 & 0xFFFF0000u);
+  const unsigned m0 = cg_pk(r0, r1), m1 = cg_pk(r2, r3);
+  const unsigned l0 = cg_pk(r0 - __builtin_bit_cast(float, m0 << 16), r1 - __builtin_bit_cast(float, m0 & 0xFFFF0000u));
+  const unsigned l1 = cg_pk(r2 - __builtin_bit_cast(float, m1 << 16), r3 - __builtin_bit_cast(float, m1 & 0xFFFF0000u));
+  return cg_u32x8{h0, h1, h0, h1, m0, m1, l0, l1};
+}
+
+__device__ __forceinline__ cg_bf16x8 cg_sub4(const cg_u32x8& c, int o) {
+  return __builtin_bit_cast(cg_bf16x8, cg_u32x4{c[o], c[o + 1], c[o + 2], c[o + 3]});
+}
+
+template <int AL, int BL, bool X3>
 struct Stage {
   f32x4 a[AL];
-  f32x4 b[BL];
+  f32x4 b[BL][X3 ? 2 : 1];  // X3: the 32-B weight chain of the thread's 4 k
 };
 
 // One BM x BN output tile (k-slice z of a split-K problem) of problem `a`; `bid` is the tile's
 // linear index (M-major over N tiles). Shared by the single-problem and the grouped kernels.
-template <int BM, int BN, int BK, int WGM, bool NCHW>
+template <int BM, int BN, int BK, int WGM, bool NCHW, bool X3 = false>
 __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, const int z) {
   using C = Cfg<BM, BN, BK, WGM>;
   constexpr int MI = C::MI, NI = C::NI, AL = C::AL, BL = C::BL, PITCH = C::PITCH;
-  constexpr int A_FLOATS = C::A_FLOATS, B_FLOATS = C::B_FLOATS;
+  constexpr int A_FLOATS = X3 ? C::A_X3 : C::A_FLOATS, B_FLOATS = X3 ? C::B_X3 : C::B_FLOATS;
+  constexpr int PX = C::PX;
   __shared__ __attribute__((aligned(16))) float smem[2 * (A_FLOATS + B_FLOATS)];
 
   const int tid = threadIdx.x;
@@ -123,8 +162,9 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
   const long long a_avail = ((long long)(a.B - b0) * a.img - a.in_co) * 4;
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void*)abase, (short)0, (int)min(a_avail, (long long)kOOB), 0x00020000);
+  constexpr unsigned kWB = X3 ? 8u : 4u;  // weight bytes per k
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.wt, (short)0, (int)min((long long)a.N * a.K * 4, (long long)kOOB), 0x00020000);
+      (void*)a.wt, (short)0, (int)min((long long)a.N * a.K * kWB, (long long)kOOB), 0x00020000);
   __shared__ int stap[16];
   if (tid < 16) stap[tid] = tid < a.ntaps ? a.tapoff[tid] : 0;
   unsigned a_row[AL];   // element offset of the row's (gy*s, gx*s) pixel, channel 0
@@ -153,7 +193,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
   for (int i = 0; i < BL; ++i) {
     const int r = srow + C::RPP * i;
     const int n = n0 + r;
-    b_row[i] = (r < BN && n < a.N) ? (unsigned)n * (unsigned)a.K * 4u : kOOB;
+    b_row[i] = (r < BN && n < a.N) ? (unsigned)n * (unsigned)a.K * kWB : kOOB;
   }
   const int nkt_all = (a.K + BK - 1) / BK;
   const int kt0 = a.ws ? z * a.kt_per : 0;
@@ -161,7 +201,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
   int kk = kt0 * BK + kq;  // absolute k of this thread's staged float4s
   __syncthreads();  // stap
 
-  auto load_tile = [&](Stage<AL, BL>& st) {
+  auto load_tile = [&](Stage<AL, BL, X3>& st) {
     // (tap, channel) of k without a divide or a data-dependent loop
     const int tap = (int)__umulhi((unsigned)kk, a.cin_magic);
     const int cc = kk - tap * a.cin;
@@ -175,23 +215,40 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
     const bool k_ok = kk < a.K;
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const unsigned off = k_ok ? b_row[i] + (unsigned)kk * 4u : kOOB;
-      st.b[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, off, 0, 0));
+      const unsigned off = k_ok ? b_row[i] + (unsigned)kk * kWB : kOOB;
+#pragma unroll
+      for (int h = 0; h < (X3 ? 2 : 1); ++h)
+        st.b[i][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, off + 16u * h, 0, 0));
     }
     kk += BK;
   };
-  auto store_tile = [&](const Stage<AL, BL>& st, int buf) {
+  auto store_tile = [&](const Stage<AL, BL, X3>& st, int buf) {
     float* As = smem + buf * (A_FLOATS + B_FLOATS);
     float* Bs = As + A_FLOATS;
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int r = srow + C::RPP * i;
-      if (C::A_FULL || r < BM) *reinterpret_cast<f32x4*>(As + r * PITCH + kq) = st.a[i];
+      if (!(C::A_FULL || r < BM)) continue;
+      if constexpr (X3) {
+        const cg_u32x8 c = cg_split_chain(st.a[i]);
+        unsigned* d = reinterpret_cast<unsigned*>(As) + r * PX + 2 * kq;
+        *reinterpret_cast<cg_u32x4*>(d) = cg_u32x4{c[0], c[1], c[2], c[3]};
+        *reinterpret_cast<cg_u32x4*>(d + 4) = cg_u32x4{c[4], c[5], c[6], c[7]};
+      } else {
+        *reinterpret_cast<f32x4*>(As + r * PITCH + kq) = st.a[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int r = srow + C::RPP * i;
-      if (C::B_FULL || r < BN) *reinterpret_cast<f32x4*>(Bs + r * PITCH + kq) = st.b[i];
+      if (!(C::B_FULL || r < BN)) continue;
+      if constexpr (X3) {
+        float* d = Bs + r * PX + 2 * kq;
+        *reinterpret_cast<f32x4*>(d) = st.b[i][0];
+        *reinterpret_cast<f32x4*>(d + 4) = st.b[i][X3 ? 1 : 0];
+      } else {
+        *reinterpret_cast<f32x4*>(Bs + r * PITCH + kq) = st.b[i][0];
+      }
     }
   };
 
@@ -204,7 +261,47 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int frow = lane & 31, fh = lane >> 5;
+  auto compute_x3 = [&](int buf) {
+    const unsigned* As = reinterpret_cast<const unsigned*>(smem + buf * (A_FLOATS + B_FLOATS));
+    const unsigned* Bs = As + A_FLOATS;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      const int q = 2 * g + fh;  // this lane half's 4 k of the 8-wide group
+      cg_u32x8 af[MI], bf[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const unsigned* p = As + (wm * C::WTM + i * 32 + frow) * PX + 8 * q;
+        const cg_u32x4 lo = *reinterpret_cast<const cg_u32x4*>(p), hi = *reinterpret_cast<const cg_u32x4*>(p + 4);
+        af[i] = cg_u32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const unsigned* p = Bs + (wn * C::WTN + j * 32 + frow) * PX + 8 * q;
+        const cg_u32x4 lo = *reinterpret_cast<const cg_u32x4*>(p), hi = *reinterpret_cast<const cg_u32x4*>(p + 4);
+        bf[j] = cg_u32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          f32x16& d = acc[i][j];
+          if constexpr (NCHW) {
+            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cg_sub4(bf[j], 2), cg_sub4(af[i], 0), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cg_sub4(bf[j], 0), cg_sub4(af[i], 2), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cg_sub4(bf[j], 0), cg_sub4(af[i], 4), d, 0, 0, 0);
+          } else {
+            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cg_sub4(af[i], 0), cg_sub4(bf[j], 2), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cg_sub4(af[i], 2), cg_sub4(bf[j], 0), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cg_sub4(af[i], 4), cg_sub4(bf[j], 0), d, 0, 0, 0);
+          }
+        }
+    }
+  };
   auto compute = [&](int buf) {
+    if constexpr (X3) {
+      compute_x3(buf);
+      return;
+    }
     const float* As = smem + buf * (A_FLOATS + B_FLOATS);
     const float* Bs = As + A_FLOATS;
 #pragma unroll
@@ -231,7 +328,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
   };
 
   // ---- main loop: loads two tiles ahead, LDS double-buffered, unrolled by 2 ---------------
-  Stage<AL, BL> s0, s1;
+  Stage<AL, BL, X3> s0, s1;
   load_tile(s0);
   if (nkt > 1) load_tile(s1);
   store_tile(s0, 0);
@@ -320,10 +417,10 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
     }
 }
 
-template <int BM, int BN, int BK, int WGM, bool NCHW>
-__global__ __launch_bounds__(256, 2) void conv_gemm_f32_kernel(const ConvArgs a) {
+template <int BM, int BN, int BK, int WGM, bool NCHW, bool X3 = false>
+__global__ __launch_bounds__(256, (X3 ? Cfg<BM, BN, BK, WGM>::BLOCKS_X3 : 2)) void conv_gemm_f32_kernel(const ConvArgs a) {
   const int tiles = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
-  conv_tile<BM, BN, BK, WGM, NCHW>(a, krrn_xcd_remap(blockIdx.x, tiles), blockIdx.y);
+  conv_tile<BM, BN, BK, WGM, NCHW, X3>(a, krrn_xcd_remap(blockIdx.x, tiles), blockIdx.y);
 }
 
 // Grouped launch: up to kMaxGroup independent problems of one tile shape in one grid (the
@@ -340,15 +437,15 @@ struct ConvGroup {
   ConvArgs p[kMaxGroup];
 };
 
-template <int BM, int BN, int BK, int WGM>
-__global__ __launch_bounds__(256, 2) void conv_group_kernel(const ConvGroup g) {
+template <int BM, int BN, int BK, int WGM, bool X3 = false>
+__global__ __launch_bounds__(256, (X3 ? Cfg<BM, BN, BK, WGM>::BLOCKS_X3 : 2)) void conv_group_kernel(const ConvGroup g) {
   const int lin = krrn_xcd_remap(blockIdx.x, g.start[g.n]);
   int q = 0;
 #pragma unroll
   for (int i = 1; i < kMaxGroup; ++i) q += (i < g.n && lin >= g.start[i]) ? 1 : 0;
   const int local = lin - g.start[q];
   const int tiles = g.tiles[q];
-  conv_tile<BM, BN, BK, WGM, false>(g.p[q], local % tiles, local / tiles);
+  conv_tile<BM, BN, BK, WGM, false, X3>(g.p[q], local % tiles, local / tiles);
 }
 
 // Sum of the split-K partials in z order + the conv epilogue (NHWC output). One thread per
@@ -390,10 +487,10 @@ __global__ __launch_bounds__(256) void splitk_epilogue_group_kernel(const ConvGr
   splitk_epilogue(g.p[q], g.splits[q], (long long)(blockIdx.x - g.estart[q]) * 256 + threadIdx.x);
 }
 
-template <int BM, int BN, int BK, int WGM, bool NCHW>
+template <int BM, int BN, int BK, int WGM, bool NCHW, bool X3 = false>
 int launch(const ConvArgs& a, int splits, hipStream_t s) {
   const int nwg = krrn_cdiv(a.M, BM) * krrn_cdiv(a.N, BN);
-  hipLaunchKernelGGL((conv_gemm_f32_kernel<BM, BN, BK, WGM, NCHW>), dim3(nwg, a.ws ? splits : 1), dim3(256), 0, s,
+  hipLaunchKernelGGL((conv_gemm_f32_kernel<BM, BN, BK, WGM, NCHW, X3>), dim3(nwg, a.ws ? splits : 1), dim3(256), 0, s,
                      a);
   if (a.ws) {
     const long long threads = (long long)a.M * (a.n_store >> 2);
@@ -403,7 +500,7 @@ int launch(const ConvArgs& a, int splits, hipStream_t s) {
   return krrn_launch_status();
 }
 
-template <int BM, int BN, int BK, int WGM>
+template <int BM, int BN, int BK, int WGM, bool X3 = false>
 int launch_group(ConvGroup& g, hipStream_t s) {
   int blocks = 0, eblocks = 0;
   for (int q = 0; q < g.n; ++q) {
@@ -419,7 +516,7 @@ int launch_group(ConvGroup& g, hipStream_t s) {
     g.start[q] = blocks;
     g.estart[q] = eblocks;
   }
-  hipLaunchKernelGGL((conv_group_kernel<BM, BN, BK, WGM>), dim3(blocks), dim3(256), 0, s, g);
+  hipLaunchKernelGGL((conv_group_kernel<BM, BN, BK, WGM, X3>), dim3(blocks), dim3(256), 0, s, g);
   if (eblocks) hipLaunchKernelGGL(splitk_epilogue_group_kernel, dim3(eblocks), dim3(256), 0, s, g);
   return krrn_launch_status();
 }
@@ -428,7 +525,7 @@ int tile_bk(int tile) { return (tile == 1 || tile == 2 || tile == 3 || tile == 5
 
 // Validate one problem and pack its kernel arguments; resolves tile 0 and the effective
 // split count (every k-slice non-empty).
-int prepare(const krrn_conv_desc& d, int& tile, ConvArgs& a, int& splits) {
+int prepare(const krrn_conv_desc& d, int& tile, ConvArgs& a, int& splits, bool x3 = false) {
   const int B = d.B, Hi = d.Hi, Wi = d.Wi, Hg = d.Hg, Wg = d.Wg, N = d.N, cin = d.cin, ntaps = d.ntaps;
   if (!d.in || !d.wt || !d.out) return KRRN_EARG;
   if (ntaps < 1 || ntaps > 9 || B < 1 || Hi < 1 || Wi < 1 || Hg < 1 || Wg < 1 || N < 1) return KRRN_ESHAPE;
@@ -462,7 +559,7 @@ int prepare(const krrn_conv_desc& d, int& tile, ConvArgs& a, int& splits) {
   // 32-bit buffer offsets: the images one tile can touch (<= 256 rows) and the weights
   const long long HWg = (long long)Hg * Wg;
   const long long span = ((256 + HWg - 1) / HWg + 1) * a.img * 4;
-  if (span >= 0xFFFFFFF0LL || (long long)N * a.K * 4 >= 0xFFFFFFF0LL) return KRRN_ESHAPE;
+  if (span >= 0xFFFFFFF0LL || (long long)N * a.K * (x3 ? 8 : 4) >= 0xFFFFFFF0LL) return KRRN_ESHAPE;
   if (tile == 0) tile = d.out_nchw ? 3 : (N <= 32 ? 6 : 8);  // same rule as runtime.conv_tile
   a.ws = nullptr;
   a.kt_per = 0;
@@ -478,30 +575,41 @@ int prepare(const krrn_conv_desc& d, int& tile, ConvArgs& a, int& splits) {
 
 }  // namespace
 
-// Tile menu (include/krrn_hip.h): 1 128x128x16, 2 128x64x16, 3 64x64x16, 4 128x128x32,
-// 5 256x32x16 (4 waves along M), 6 128x32x32 (4 waves along M), 7 128x64x32, 8 64x64x32.
-KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin,
-                             int Hg, int Wg, int in_s, int ntaps, const int* tap_dy, const int* tap_dx,
-                             const float* wt, int N, int n_store, const float* scale, const float* bias,
-                             const float* bias2, int b2_div, const float* res, int res_cs, int res_co,
-                             float* out, int out_cs, int out_co, int Ho, int Wo, int osy, int osx, int ooy,
-                             int oox, int relu, int out_nchw, int tile, int splits, float* workspace,
-                             void* stream) {
+namespace {
+int conv2d(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin, int Hg, int Wg, int in_s, int ntaps,
+           const int* tap_dy, const int* tap_dx, const void* wt, int N, int n_store, const float* scale,
+           const float* bias, const float* bias2, int b2_div, const float* res, int res_cs, int res_co, float* out,
+           int out_cs, int out_co, int Ho, int Wo, int osy, int osx, int ooy, int oox, int relu, int out_nchw,
+           int tile, int splits, float* workspace, bool x3, void* stream) {
   if (!tap_dy || !tap_dx) return KRRN_EARG;
   if (ntaps < 1 || ntaps > 9) return KRRN_ESHAPE;
   krrn_conv_desc d;
   d.in = in; d.in_cs = in_cs; d.in_co = in_co; d.B = B; d.Hi = Hi; d.Wi = Wi; d.cin = cin;
   d.Hg = Hg; d.Wg = Wg; d.in_s = in_s; d.ntaps = ntaps;
   for (int t = 0; t < 9; ++t) { d.tap_dy[t] = t < ntaps ? tap_dy[t] : 0; d.tap_dx[t] = t < ntaps ? tap_dx[t] : 0; }
-  d.wt = wt; d.N = N; d.n_store = n_store; d.scale = scale; d.bias = bias; d.bias2 = bias2; d.b2_div = b2_div;
+  d.wt = reinterpret_cast<const float*>(wt); d.N = N; d.n_store = n_store; d.scale = scale; d.bias = bias;
+  d.bias2 = bias2; d.b2_div = b2_div;
   d.res = res; d.res_cs = res_cs; d.res_co = res_co; d.out = out; d.out_cs = out_cs; d.out_co = out_co;
   d.Ho = Ho; d.Wo = Wo; d.osy = osy; d.osx = osx; d.ooy = ooy; d.oox = oox; d.relu = relu;
   d.out_nchw = out_nchw; d.splits = splits; d.workspace = workspace;
   ConvArgs a;
   int sp = 1;
-  const int st = prepare(d, tile, a, sp);
+  const int st = prepare(d, tile, a, sp, x3);
   if (st != KRRN_OK) return st;
   hipStream_t s = (hipStream_t)stream;
+  if (x3) {  // NHWC output
+    if (out_nchw) return KRRN_EARG;
+    switch (tile) {
+      case 1: return launch<128, 128, 16, 2, false, true>(a, sp, s);
+      case 2: return launch<128, 64, 16, 2, false, true>(a, sp, s);
+      case 3: return launch<64, 64, 16, 2, false, true>(a, sp, s);
+      case 4: return launch<128, 128, 32, 2, false, true>(a, sp, s);
+      case 5: return launch<256, 32, 16, 4, false, true>(a, sp, s);
+      case 6: return launch<128, 32, 32, 4, false, true>(a, sp, s);
+      case 7: return launch<128, 64, 32, 2, false, true>(a, sp, s);
+      default: return launch<64, 64, 32, 2, false, true>(a, sp, s);
+    }
+  }
   if (out_nchw) {
     // narrow heads (mask/region/xyz logits, 3C normals): 32-wide N tiles waste least MFMA work
     if (tile == 6) return launch<128, 32, 32, 4, true>(a, 1, s);
@@ -520,20 +628,61 @@ KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int H
     default: return launch<64, 64, 32, 2, false>(a, sp, s);
   }
 }
+}  // namespace
 
-KRRN_API int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* stream) {
+// Tile menu (include/krrn_hip.h): 1 128x128x16, 2 128x64x16, 3 64x64x16, 4 128x128x32,
+// 5 256x32x16 (4 waves along M), 6 128x32x32 (4 waves along M), 7 128x64x32, 8 64x64x32.
+KRRN_API int krrn_conv2d_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin,
+                             int Hg, int Wg, int in_s, int ntaps, const int* tap_dy, const int* tap_dx,
+                             const float* wt, int N, int n_store, const float* scale, const float* bias,
+                             const float* bias2, int b2_div, const float* res, int res_cs, int res_co,
+                             float* out, int out_cs, int out_co, int Ho, int Wo, int osy, int osx, int ooy,
+                             int oox, int relu, int out_nchw, int tile, int splits, float* workspace,
+                             void* stream) {
+  return conv2d(in, in_cs, in_co, B, Hi, Wi, cin, Hg, Wg, in_s, ntaps, tap_dy, tap_dx, wt, N, n_store, scale, bias,
+                bias2, b2_div, res, res_cs, res_co, out, out_cs, out_co, Ho, Wo, osy, osx, ooy, oox, relu, out_nchw,
+                tile, splits, workspace, false, stream);
+}
+
+KRRN_API int krrn_conv2d_x3_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin, int Hg,
+                                int Wg, int in_s, int ntaps, const int* tap_dy, const int* tap_dx, const void* wt3,
+                                int N, int n_store, const float* scale, const float* bias, const float* bias2,
+                                int b2_div, const float* res, int res_cs, int res_co, float* out, int out_cs,
+                                int out_co, int Ho, int Wo, int osy, int osx, int ooy, int oox, int relu, int tile,
+                                int splits, float* workspace, void* stream) {
+  return conv2d(in, in_cs, in_co, B, Hi, Wi, cin, Hg, Wg, in_s, ntaps, tap_dy, tap_dx, wt3, N, n_store, scale, bias,
+                bias2, b2_div, res, res_cs, res_co, out, out_cs, out_co, Ho, Wo, osy, osx, ooy, oox, relu, 0, tile,
+                splits, workspace, true, stream);
+}
+
+namespace {
+int conv_group(const krrn_conv_desc* descs, int n, int tile, bool x3, void* stream) {
   if (!descs) return KRRN_EARG;
   if (n < 1 || n > kMaxGroup) return KRRN_ESHAPE;
-  if (tile != 6 && tile != 8) return KRRN_EARG;
+  if (tile != 1 && tile != 6 && tile != 8) return KRRN_EARG;
   ConvGroup g;
   g.n = n;
   for (int q = 0; q < n; ++q) {
     if (descs[q].out_nchw) return KRRN_EARG;
     int t = tile;
-    const int st = prepare(descs[q], t, g.p[q], g.splits[q]);
+    const int st = prepare(descs[q], t, g.p[q], g.splits[q], x3);
     if (st != KRRN_OK) return st;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (x3) {
+    if (tile == 1) return launch_group<128, 128, 16, 2, true>(g, s);
+    return tile == 6 ? launch_group<128, 32, 32, 4, true>(g, s) : launch_group<64, 64, 32, 2, true>(g, s);
+  }
+  if (tile == 1) return launch_group<128, 128, 16, 2>(g, s);
   if (tile == 6) return launch_group<128, 32, 32, 4>(g, s);
   return launch_group<64, 64, 32, 2>(g, s);
+}
+}  // namespace
+
+KRRN_API int krrn_conv2d_group_f32(const krrn_conv_desc* descs, int n, int tile, void* stream) {
+  return conv_group(descs, n, tile, false, stream);
+}
+
+KRRN_API int krrn_conv2d_group_x3_f32(const krrn_conv_desc* descs, int n, int tile, void* stream) {
+  return conv_group(descs, n, tile, true, stream);
 }

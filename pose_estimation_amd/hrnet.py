@@ -45,6 +45,8 @@ SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
 GEMM_1X1 = os.environ.get("KRRN_GEMM_1X1", "1") == "1"
 # Winograd convs on the bf16 matrix cores with f32-accurate split operands (krrn_conv3x3_wino_x3_f32)
 WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
+# implicit-GEMM convs (transposed convs, stem / transitions) likewise (krrn_conv2d[_group]_x3_f32)
+CONV_X3 = os.environ.get("KRRN_CONV_X3", "1") == "1"
 
 BN_MOMENTUM = 0.1
 
@@ -304,19 +306,31 @@ class _Builder:
                           out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=2, osx=2, ooy=ooy,
                           oox=oox, relu=relu, cin=spec.cin, cout=spec.cout)
                      for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off))]
-            add_conv_group(self.plan, probs, tile=CONVT_GROUP_TILE, tag=tag + "_convT")
+            x3 = CONV_X3
+            if x3:
+                for pr, cls in zip(probs, range(len(probs))):
+                    w3 = ops.conv_weights_x3(spec.wt[cls])
+                    self.specs.append(w3)
+                    pr["wt"] = ptr(w3)
+            # split-bf16: the 128x128x16 tile (profiles/bench_conv_x3.py: transposed 4x4 272 -> 128 at
+            # 30 px 501 us, 3x3 128 -> 128 at 60 px 665 us, against 742 / 854 for the f32 64x64x32)
+            add_conv_group(self.plan, probs, tile=1 if x3 else CONVT_GROUP_TILE, tag=tag + "_convT", x3=x3)
             return
         for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off)):
             if spec.kind == "conv":
                 Hg, Wg, in_s, osy, osx = out.H, out.W, spec.stride, 1, 1
             else:
                 Hg, Wg, in_s, osy, osx = x.H, x.W, 1, 2, 2
+            w3 = None
+            if CONV_X3:
+                w3 = ops.conv_weights_x3(spec.wt[cls])
+                self.specs.append(w3)
             add_conv(self.plan, x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=Hg,
                      Wg=Wg, in_s=in_s, taps=taps, wt=ptr(spec.wt[cls]), N=np_, n_store=np_, scale=ptr(spec.scale),
                      bias=ptr(spec.bias), res=ptr(res.t) if res is not None else None,
                      res_cs=res.cs if res is not None else 0, res_co=res.co if res is not None else 0,
                      out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=osy, osx=osx, ooy=ooy,
-                     oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag)
+                     oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag, wt3=ptr(w3) if w3 is not None else None)
 
     def small_grouped(self, xs: List[Act], convs: List[Tuple[nn.Module, nn.Module]], res: Optional[List[Act]],
                       tag: str) -> Optional[List[Act]]:

@@ -95,8 +95,9 @@ def conv_out_hw(spec: ConvSpec, H: int, W: int) -> Tuple[int, int]:
 
 def conv2d(x: Act, spec: ConvSpec, out: Act, res: Optional[Act] = None, relu: bool = False,
            bias2: Optional[torch.Tensor] = None, b2_div: int = 1, tile: int = 0, splits: int = 1,
-           ws: Optional[torch.Tensor] = None):
-    """out = act(BN(conv(x)) [+ bias2] [+ res]) written into ``out``'s channel slice."""
+           ws: Optional[torch.Tensor] = None, x3: bool = False):
+    """out = act(BN(conv(x)) [+ bias2] [+ res]) written into ``out``'s channel slice; x3: on the
+    bf16 matrix cores with split operands (krrn_conv2d_x3_f32, tiles 6 / 7 / 8)."""
     assert x.cp == spec.cin_p, (x.c, x.cp, spec.cin_p)
     Ho, Wo = out.H, out.W
     np_ = pad4(spec.cout)
@@ -107,6 +108,20 @@ def conv2d(x: Act, spec: ConvSpec, out: Act, res: Optional[Act] = None, relu: bo
             Hg, Wg, in_s, osy, osx = x.H, x.W, 1, 2, 2
         dy = _int_array([t[0] for t in taps])
         dx = _int_array([t[1] for t in taps])
+        if x3:
+            from .runtime import conv_tile
+            t = tile or conv_tile(x.B * Hg * Wg, np_, spec.cin_p * len(taps))
+            if not hasattr(spec, "wt3"):
+                spec.wt3 = [conv_weights_x3(w) for w in spec.wt]
+            w3 = spec.wt3[cls]
+            _lib.call("krrn_conv2d_x3_f32",
+                      _ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, Hg, Wg, in_s, len(taps), dy, dx,
+                      _ptr(w3), np_, np_, _ptr(spec.scale), _ptr(spec.bias), _ptr(bias2), b2_div,
+                      _ptr(res.t if res is not None else None), res.cs if res is not None else 0,
+                      res.co if res is not None else 0,
+                      _ptr(out.t), out.cs, out.co, Ho, Wo, osy, osx, ooy, oox, int(relu), t, splits,
+                      _ptr(ws), _stream())
+            continue
         _lib.call("krrn_conv2d_f32",
                   _ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p,
                   Hg, Wg, in_s, len(taps), dy, dx,
@@ -247,6 +262,15 @@ def wino_weights_x3(U: torch.Tensor) -> torch.Tensor:
     h, m, l = (t.reshape(nck, 16, N, 2, 4) for t in (h, m, l))
     mh = torch.cat([m, h], dim=-1).reshape(-1)
     return torch.cat([mh, l.reshape(-1)]).contiguous()
+
+
+def conv_weights_x3(wt: torch.Tensor) -> torch.Tensor:
+    """krrn_conv2d_f32 weights [N][K] f32 -> the split chains krrn_conv2d_x3_f32 reads: bf16
+    [N][K / 4][16], per 4 k the terms m0..m3 h0..h3 l0..l3 then 4 zeros (K a multiple of 4)."""
+    N, K = wt.shape
+    h, m, l = split_bf16x3(wt)
+    h, m, l = (t.reshape(N, K // 4, 4) for t in (h, m, l))
+    return torch.cat([m, h, l, torch.zeros_like(l)], dim=-1).contiguous()
 
 
 def wino_eligible(spec: ConvSpec, M: int) -> bool:

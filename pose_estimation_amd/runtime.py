@@ -42,6 +42,9 @@ _lib.register("krrn_randperm_i32", [P, U, I, I, I, P, P])
 _lib.register("krrn_ransac_subsets", [P, U, I, I, I, P, P])
 _lib.register("krrn_rng_advance", [P, P])
 _lib.register("krrn_conv2d_group_f32", [P, I, I, P])
+_lib.register("krrn_conv2d_group_x3_f32", [P, I, I, P])
+_lib.register("krrn_conv2d_x3_f32", [P, I, I, I, I, I, I, I, I, I, I, P, P, P, I, I, P, P, P, I, P, I, I, P, I, I, I, I,
+                                     I, I, I, I, I, I, I, P, P])
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_wino_variant", [I])
 _lib.register("krrn_conv3x3_wino_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
@@ -266,11 +269,19 @@ def _iarr(vals):
     return arr
 
 
+# split-bf16 implicit GEMM (krrn_conv2d_x3_f32): 128x64x16 tiles for N > 32, no split-K
+# (profiles/bench_conv_x3.py, B = 64: 3x3 / s2 64 -> 64 at 120 px 185 us against the f32 kernel's
+# best 206; the 64x64x32 tile is slower in x3: 245 us, its 32x32 wave tiles LDS-bound)
+X3_TILE = 2
+
+
 def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_store, scale, bias,
              bias2=None, b2_div=1, res=None, res_cs=0, res_co=0, out, out_cs, out_co, Ho, Wo, osy=1, osx=1, ooy=0,
-             oox=0, relu=False, nchw=False, cin=None, cout=None, tag="", tile=None, splits=None):
-    """Append one krrn_conv2d_f32 launch. Pointers are ctypes values (see `ptr`). cin/cout are the
-    logical channel counts used for the algorithmic FLOP count 2*cin*cout*ntaps*M."""
+             oox=0, relu=False, nchw=False, cin=None, cout=None, tag="", tile=None, splits=None, wt3=None):
+    """Append one krrn_conv2d_f32 launch, or krrn_conv2d_x3_f32 (split-bf16 operands, f32 accuracy)
+    when `wt3` (ops.conv_weights_x3 of the weights) is given and the tile allows. Pointers are
+    ctypes values (see `ptr`). cin/cout are the logical channel counts used for the algorithmic
+    FLOP count 2*cin*cout*ntaps*M."""
     M = B * Hg * Wg
     K = cin_p * len(taps)
     if tile is None and tag and os.environ.get(f"KRRN_TILE_{tag.upper()}"):  # tile-menu experiments
@@ -282,12 +293,24 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
     cin = cin_p if cin is None else cin
     cout = n_store if cout is None else cout
     flops = 2.0 * cin * cout * len(taps) * M
+    kname = CONV_KERNELS[tile] + (",nchw" if nchw else "") + (",splitk" if splits > 1 else "")
+    if wt3 is not None and not nchw and N > 32 and splits == 1:
+        tile = X3_TILE
+        # matrix pipe: 6 bf16 term products per f32 product at 16x the f32 rate (f32-MFMA time)
+        kname = CONV_KERNELS[tile]
+        plan.add("krrn_conv2d_x3_f32", x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, len(taps),
+                 _iarr([t[0] for t in taps]), _iarr([t[1] for t in taps]), wt3, N, n_store, scale, bias,
+                 bias2 if bias2 is not None else P(0), b2_div, res if res is not None else P(0), res_cs, res_co, out,
+                 out_cs, out_co, Ho, Wo, osy, osx, ooy, oox, int(relu), tile, splits, ptr(ws),
+                 meta=dict(kernel=kname.replace("conv_gemm_f32", "conv_gemm_x3"), flops=flops, tag=tag, M=M, N=N,
+                           K=K, splits=splits, mfma_flops=2.0 * M * N * K * 6 / 16,
+                           mfma_bf16_flops=2.0 * M * N * K * 6))
+        return
     plan.add("krrn_conv2d_f32", x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, len(taps), _iarr([t[0] for t in taps]),
              _iarr([t[1] for t in taps]), wt, N, n_store, scale, bias, bias2 if bias2 is not None else P(0), b2_div,
              res if res is not None else P(0), res_cs, res_co, out, out_cs, out_co, Ho, Wo, osy, osx, ooy, oox,
              int(relu), int(nchw), tile, splits, ptr(ws),
-             meta=dict(kernel=CONV_KERNELS[tile] + (",nchw" if nchw else "") + (",splitk" if splits > 1 else ""),
-                       flops=flops, tag=tag, M=M, N=N, K=K, splits=splits))
+             meta=dict(kernel=kname, flops=flops, tag=tag, M=M, N=N, K=K, splits=splits))
 
 
 GROUP_TILE = int(os.environ.get("KRRN_GROUP_TILE", "6"))
@@ -337,9 +360,10 @@ def conv_desc(*, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_s
     return d
 
 
-def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str = "group"):
+def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str = "group", x3: bool = False):
     """One krrn_conv2d_group_f32 launch over up to 4 independent convs (dicts of conv_desc
-    keyword arguments plus 'cin' / 'cout' logical channels for the FLOP count)."""
+    keyword arguments plus 'cin' / 'cout' logical channels for the FLOP count), or
+    krrn_conv2d_group_x3_f32 (x3: every problem's `wt` is ops.conv_weights_x3 chains)."""
     tile = GROUP_TILE if tile is None else tile
     n = len(problems)
     arr = (ConvDesc * n)()
@@ -358,9 +382,12 @@ def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str 
         nsplit = max(nsplit, sp)
         shapes.append((M, pr["N"], K, sp))
     plan.buffers.append(arr)
-    plan.add("krrn_conv2d_group_f32", ctypes.cast(arr, P), n, tile,
-             meta=dict(kernel=f"conv_group<{','.join(map(str, TILE_SHAPES[tile]))}>", flops=flops, tag=tag,
-                       M=shapes[0][0], N=shapes[0][1], K=shapes[0][2], splits=nsplit, shapes=shapes))
+    meta = dict(kernel=f"conv_group{'_x3' if x3 else ''}<{','.join(map(str, TILE_SHAPES[tile]))}>", flops=flops,
+                tag=tag, M=shapes[0][0], N=shapes[0][1], K=shapes[0][2], splits=nsplit, shapes=shapes)
+    if x3:
+        pipe = sum(2.0 * M * N * K for M, N, K, _ in shapes)
+        meta.update(mfma_flops=pipe * 6 / 16, mfma_bf16_flops=pipe * 6)
+    plan.add("krrn_conv2d_group_x3_f32" if x3 else "krrn_conv2d_group_f32", ctypes.cast(arr, P), n, tile, meta=meta)
 
 
 BLAS = os.environ.get("KRRN_BLAS", "1") == "1"

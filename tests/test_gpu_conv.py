@@ -108,6 +108,46 @@ def test_convT(dev, cin, cout, k, p, op, H):
     torch.testing.assert_close(got, ref, **TOL)
 
 
+@pytest.mark.parametrize("cin,cout,k,s,H,tile,splits,kind", [
+    (64, 64, 3, 2, 60, 2, 1, "conv"), (18, 36, 3, 1, 15, 6, 1, "conv"), (270, 132, 3, 1, 17, 8, 1, "conv"),
+    (144, 144, 3, 1, 4, 8, 10, "conv"), (36, 20, 1, 1, 13, 7, 1, "conv"), (130, 64, 4, 1, 9, 1, 1, "convT"),
+    (128, 72, 3, 1, 7, 4, 1, "convT"), (40, 132, 3, 1, 11, 3, 1, "conv"), (20, 24, 3, 2, 23, 5, 1, "conv")])
+def test_conv_x3(dev, cin, cout, k, s, H, tile, splits, kind):
+    """krrn_conv2d_x3_f32 (split-bf16 operands): the f32 tolerance against torch, within f32
+    accumulation noise of the f32 kernel, pad channels zero; odd sizes, residual, split-K,
+    transposed-conv parity classes."""
+    g = torch.Generator().manual_seed(cin * 3 + cout + k)
+    B = 3
+    if kind == "conv":
+        conv = nn.Conv2d(cin, cout, k, s, (k - 1) // 2, bias=True)
+    else:
+        conv = nn.ConvTranspose2d(cin, cout, k, 2, 1, output_padding=1 if k == 3 else 0, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+        conv.bias.copy_(0.1 * torch.randn(cout, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, H, generator=g)
+    y = bn(conv(x))
+    res = torch.randn(y.shape, generator=g)
+    ref = torch.relu(y + res).detach()
+    spec = ops.make_conv(conv, bn, dev) if kind == "conv" else ops.make_convT(conv, bn, dev)
+    xa = _nhwc(x, dev)
+    Ho, Wo = ref.shape[2:]
+    ra = _nhwc(res, dev)
+    outs = []
+    for x3 in (False, True):
+        out = ops.new_act(B, Ho, Wo, cout, dev, cs=ops.pad4(cout) + 4)
+        out.t[..., :ops.pad4(cout)] = float("nan")
+        ws = torch.empty(splits * B * Ho * Wo * ops.pad4(cout), device=dev) if splits > 1 else None
+        ops.conv2d(xa, spec, out, res=ra, relu=True, tile=tile, splits=splits, ws=ws, x3=x3)
+        torch.cuda.synchronize()
+        outs.append(out.t.clone())
+    f32, x3 = (o[..., :cout].permute(0, 3, 1, 2).cpu() for o in outs)
+    torch.testing.assert_close(x3, ref, **TOL)
+    torch.testing.assert_close(x3, f32, rtol=1e-5, atol=2e-6 * float(ref.abs().max()))
+    assert torch.count_nonzero(outs[1][..., ops.pad4(cout):]).item() == 0
+
+
 @pytest.mark.parametrize("cout", [70, 3, 130])
 def test_conv_nchw_out(dev, cout):
     g = torch.Generator().manual_seed(5)
@@ -140,10 +180,10 @@ def test_gemm_bias2(dev):
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("tile", [6, 8])
-def test_conv_group_matches_single(dev, tile):
-    """krrn_conv2d_group_f32 over the four HRNet-W18 branch shapes (incl. split-K members) gives
-    bit-identical results to the same problems launched one by one."""
+@pytest.mark.parametrize("tile,x3", [(6, False), (8, False), (1, False), (6, True), (8, True), (1, True)])
+def test_conv_group_matches_single(dev, tile, x3):
+    """krrn_conv2d_group_f32 (x3: krrn_conv2d_group_x3_f32) over the four HRNet-W18 branch shapes
+    (incl. split-K members) gives bit-identical results to the same problems launched one by one."""
     import ctypes
     from pose_estimation_amd import _lib
     from pose_estimation_amd.runtime import P, add_conv_group, conv_splits, Plan, ptr
@@ -166,14 +206,15 @@ def test_conv_group_matches_single(dev, tile):
         M, K = B * H * H, spec.cin_p * 9
         sp = conv_splits(M, ops.pad4(c), K, tile)
         ws = torch.empty(max(1, sp) * M * ops.pad4(c), device=dev)
-        ops.conv2d(xa, spec, ref, res=ra, relu=True, tile=tile, splits=sp, ws=ws)
+        ops.conv2d(xa, spec, ref, res=ra, relu=True, tile=tile, splits=sp, ws=ws, x3=x3)
+        w = ops.conv_weights_x3(spec.wt[0]) if x3 else spec.wt[0]
         probs.append(dict(x=ptr(xa.t), x_cs=xa.cs, x_co=0, B=B, Hi=H, Wi=H, cin_p=spec.cin_p, Hg=H, Wg=H, in_s=1,
-                          taps=spec.taps[0], wt=ptr(spec.wt[0]), N=ops.pad4(c), n_store=ops.pad4(c),
+                          taps=spec.taps[0], wt=ptr(w), N=ops.pad4(c), n_store=ops.pad4(c),
                           scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(ra.t), res_cs=ra.cs, res_co=0,
                           out=ptr(out.t), out_cs=out.cs, out_co=0, Ho=H, Wo=H, relu=True, cin=c, cout=c))
         outs.append(out)
-        refs.append((ref, spec, xa, ra))
-    add_conv_group(plan, probs, tile=tile)
+        refs.append((ref, spec, xa, ra, w))
+    add_conv_group(plan, probs, tile=tile, x3=x3)
     plan.run({})
     torch.cuda.synchronize()
     for out, (ref, *_keep) in zip(outs, refs):
