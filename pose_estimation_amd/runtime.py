@@ -284,6 +284,7 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
     FLOP count 2*cin*cout*ntaps*M."""
     M = B * Hg * Wg
     K = cin_p * len(taps)
+    tile_req = tile
     if tile is None and tag and os.environ.get(f"KRRN_TILE_{tag.upper()}"):  # tile-menu experiments
         tile = int(os.environ[f"KRRN_TILE_{tag.upper()}"])
     tile = conv_tile(M, N, K, nchw) if tile is None else tile
@@ -295,7 +296,7 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
     flops = 2.0 * cin * cout * len(taps) * M
     kname = CONV_KERNELS[tile] + (",nchw" if nchw else "") + (",splitk" if splits > 1 else "")
     if wt3 is not None and not nchw and N > 32 and splits == 1:
-        tile = X3_TILE
+        tile = X3_TILE if tile_req is None else tile_req
         # matrix pipe: 6 bf16 term products per f32 product at 16x the f32 rate (f32-MFMA time)
         kname = CONV_KERNELS[tile]
         plan.add("krrn_conv2d_x3_f32", x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, len(taps),

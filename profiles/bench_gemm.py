@@ -1,12 +1,13 @@
 """Micro-bench: krrn_conv2d_f32 as a plain GEMM (the GCN `feature_map @ weights` and TBase shapes)
 over the tile menu, vs hipBLASLt (torch.mm, f32). usage: python3 profiles/bench_gemm.py
-env SHAPES="M,K,N[,a_cs];..." TILES="1,2,..." """
+env SHAPES="M,K,N[,a_cs];..." TILES="1,2,..." X3=1 """
 import os
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pose_estimation_amd import ops  # noqa: E402
 from pose_estimation_amd.runtime import TILE_SHAPES, Plan, add_conv, ptr  # noqa: E402
 
 dev = torch.device("cuda", 0)
@@ -14,6 +15,7 @@ shapes = [(64000, 128, 1024, 384), (16000, 128, 1024, 384), (3968, 384, 4096, 38
 if os.environ.get("SHAPES"):
     shapes = [tuple(int(v) for v in t.split(",")) for t in os.environ["SHAPES"].split(";")]
 tiles = [int(t) for t in os.environ.get("TILES", ",".join(str(k) for k in TILE_SHAPES)).split(",")]
+X3 = os.environ.get("X3") == "1"  # also krrn_conv2d_x3_f32 (split-bf16 operands) per tile
 
 
 def ev_time(fn, reps=20):
@@ -39,15 +41,18 @@ for shp in shapes:
     ref = A[:, :K] @ W.t()
     fl = 2.0 * M * N * K
     line = [f"M{M} K{K} N{N}:"]
+    W3 = ops.conv_weights_x3(W)
     for t in tiles:
-        out = torch.zeros(M, N, device=dev)
-        plan = Plan(dev)
-        add_conv(plan, x=ptr(A), x_cs=a_cs, x_co=0, B=1, Hi=1, Wi=M, cin_p=K, Hg=1, Wg=M, in_s=1, taps=[(0, 0)],
-                 wt=ptr(W), N=N, n_store=N, scale=ptr(scale), bias=ptr(bias), out=ptr(out), out_cs=N, out_co=0, Ho=1,
-                 Wo=M, tile=t, splits=1)
-        ms = ev_time(lambda: plan.run({}))
-        err = float((out - ref).abs().max() / ref.abs().max())
-        line.append(f"t{t}{TILE_SHAPES[t]} {ms*1e3:.1f}us {fl/ms/1e9:.0f}TF" + (" ERR" if err > 1e-5 else ""))
+        for x3 in ((False, True) if X3 else (False,)):
+            out = torch.zeros(M, N, device=dev)
+            plan = Plan(dev)
+            add_conv(plan, x=ptr(A), x_cs=a_cs, x_co=0, B=1, Hi=1, Wi=M, cin_p=K, Hg=1, Wg=M, in_s=1, taps=[(0, 0)],
+                     wt=ptr(W), N=N, n_store=N, scale=ptr(scale), bias=ptr(bias), out=ptr(out), out_cs=N, out_co=0,
+                     Ho=1, Wo=M, tile=t, splits=1, wt3=ptr(W3) if x3 else None)
+            ms = ev_time(lambda: plan.run({}))
+            err = float((out - ref).abs().max() / ref.abs().max())
+            line.append(f"{'x3 ' if x3 else ''}t{t}{TILE_SHAPES[t]} {ms*1e3:.1f}us {fl/ms/1e9:.0f}TF"
+                        + (" ERR" if err > 1e-5 else ""))
     from pose_estimation_amd import _lib
     from pose_estimation_amd.runtime import P
     st = P(torch.cuda.current_stream().cuda_stream)
