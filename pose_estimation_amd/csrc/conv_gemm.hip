@@ -17,7 +17,10 @@
 // Numerics: operands stay f32 and are multiplied on v_mfma_f32_32x32x2_f32, which is
 // bit-for-bit a k-ordered fmaf chain (cdna_hip_programming.md §3 "FP32-input MFMA").
 // The reference path evaluates in f32 (tools/trainer.py:466-475 has no autocast at
-// eval), so this is the reference precision, not a reduced one.
+// eval), so this is the reference precision, not a reduced one. The X3 instantiations
+// (krrn_conv2d_x3_f32 / krrn_conv2d_group_x3_f32) keep that accuracy on the bf16 matrix cores:
+// both operands split into three exact bf16 terms, six term products per f32 product, f32
+// accumulation (see "split-bf16 operands" below); the transposed-conv groups run there.
 //
 // Tiling (MI355X-first):
 //   * block = 256 threads = 4 waves laid out WGM (along M) x 4/WGM (along N); block tile
