@@ -43,6 +43,8 @@ CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
 SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
 # wide 1x1 convs as hipBLASLt GEMMs
 GEMM_1X1 = os.environ.get("KRRN_GEMM_1X1", "1") == "1"
+# fuse-layer sums opened by the identity term (no add_relu launches; _fuse_output)
+FUSE_ID_FIRST = os.environ.get("KRRN_FUSE_ID_FIRST", "1") == "1"
 # Winograd convs on the bf16 matrix cores with f32-accurate split operands (krrn_conv3x3_wino_x3_f32)
 WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
 # implicit-GEMM convs (transposed convs, stem / transitions) likewise (krrn_conv2d[_group]_x3_f32)
@@ -419,11 +421,16 @@ class _Builder:
         return fused
 
     def _fuse_output(self, ys: List[Act], m: HighResolutionModule, i: int, out: Optional[Act]) -> Act:
+        """relu(sum_j fuse_layers[i][j](ys[j])) (myhrnet.py:232-248). With FUSE_ID_FIRST the identity
+        term opens the sum (read in place) and every other term adds it in its producer's epilogue
+        (conv residual / resize add), so no separate add launch exists; the f32 summation order then
+        differs from the reference's j order (rounding-level)."""
         nb = m.num_branches
         out = out if out is not None else self.act(ys[i].H, ys[i].W, ys[i].c)
         acc: Optional[Act] = None  # running sum lives in `out` once written
-        for j in range(nb):
-            last = j == nb - 1
+        order = ([i] + [j for j in range(nb) if j != i]) if FUSE_ID_FIRST else list(range(nb))
+        for pos, j in enumerate(order):
+            last = pos == nb - 1
             if j == i:
                 if acc is None:
                     acc = ys[i]  # identity term: read in place, no copy
