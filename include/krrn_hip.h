@@ -115,6 +115,17 @@ int krrn_blas_gemm_run(const krrn_blas_gemm* g, const float* a, const float* w, 
                        float* out, void* workspace, long long ws_bytes, void* stream);
 int krrn_blas_gemm_destroy(krrn_blas_gemm* g);
 
+/* The same GEMM on the bf16 matrix cores at f32 accuracy (gemm_x3.hip: split-bf16 operands,
+ * six term products per f32 product): the GCN `feature_map @ weights` of G6/G7
+ * (lib/network/point/gcn3d.py:125-127, 184-186) and TBase's Conv1d chain (posenet.py:51-96).
+ *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n][k] + bias[n] + res[m*ldr + n])
+ * in `batch` strided groups of M rows (a_grp / o_grp / r_grp floats per group). w3f holds W split
+ * into per-wave MFMA fragments (ops.gemm_weights_x3: [N/32][K/8][2][64 lanes][4] u32).
+ * K % 32 == 0, N % 128 == 0, lda / ldo / ldr % 4 == 0, 16-byte aligned A / W / out / res. */
+int krrn_gemm_x3_f32(const float* a, int lda, int M, int K, int N, const void* w3f, const float* bias,
+                     const float* res, int ldr, float* out, int ldo, int relu, int batch, long long a_grp,
+                     long long o_grp, long long r_grp, void* stream);
+
 /* 1x1 conv with NCHW output (the heads' final xyz / normal convs, lib/network/krrn.py:97-98,
  * 80-84): out[b][out_co + n][p] = scale[n] * sum_c in[(b * HW + p) * in_cs + in_co + c] wt[n][c]
  * + bias[n] for n < n_store, p < HW; out has out_cs channels per image. cin <= 256 (multiple of 4),

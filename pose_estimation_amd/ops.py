@@ -273,6 +273,19 @@ def conv_weights_x3(wt: torch.Tensor) -> torch.Tensor:
     return torch.cat([m, h, l, torch.zeros_like(l)], dim=-1).contiguous()
 
 
+def gemm_weights_x3(wt: torch.Tensor) -> torch.Tensor:
+    """GEMM weights [N][K] f32 (scale folded) -> the wave fragments krrn_gemm_x3_f32 reads: int32
+    [N/32][K/8][2][64][4]. Fragment (column block nb, 8-k group g, quad q) is one coalesced 1-KB
+    wave load: lane fh*32 + nl holds, for column 32 nb + nl and k = 8 g + 4 fh .. + 3, the MFMA
+    operand quad q of the split terms: q = 0 [h0..h3 l0..l3] (pairs with the activations' [h h]),
+    q = 1 [m0..m3 h0..h3] (pairs with [h m] and [m l]). N % 32 == 0, K % 8 == 0."""
+    N, K = wt.shape
+    h, m, l = (t.reshape(N, K // 4, 4) for t in split_bf16x3(wt))
+    c = torch.cat([h, l, m, h], dim=-1).contiguous()  # [N][K/4][16] bf16 = P0 | P1
+    c = c.view(torch.int32).reshape(N // 32, 32, K // 8, 2, 2, 4)  # nb nl g fh q 4
+    return c.permute(0, 2, 4, 3, 1, 5).contiguous()                 # nb g q fh nl 4
+
+
 def wino_eligible(spec: ConvSpec, M: int) -> bool:
     """Fused Winograd for the wide stride-1 3x3 convs (>= 32 channels in and out, >= 32k output
     pixels); the narrow HRNet branches stay on the implicit GEMM (latency-bound there)."""

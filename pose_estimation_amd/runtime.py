@@ -17,7 +17,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib, ops
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -54,6 +54,7 @@ _lib.register("krrn_conv_small_group_f32", [P, I, P])
 _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L, P, P])
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])
+_lib.register("krrn_gemm_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, L, L, L, P])
 
 
 class ConvDesc(ctypes.Structure):
@@ -393,6 +394,11 @@ def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str 
 
 BLAS = os.environ.get("KRRN_BLAS", "1") == "1"
 BLAS_MAX_WS = 64 << 20
+# plain GEMMs with K >= GEMM_X3_MINK on gemm_x3.hip (split-bf16), the rest on hipBLASLt: measured
+# (profiles/bench_gemm.py, MI355X) 10-18 % faster at K = 256..1024, no faster at K = 128 (the
+# level-0/1 GCN GEMMs: output-write-bound, 262 MB per launch)
+GEMM_X3 = os.environ.get("KRRN_GEMM_X3", "1") == "1"
+GEMM_X3_MINK = int(os.environ.get("KRRN_GEMM_X3_MINK", "256"))
 
 
 class _BlasPlan:
@@ -423,6 +429,17 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
     if scale is not None:
         w = w * scale.reshape(N, 1).to(w.device)
     w = w.contiguous()
+    flops = 2.0 * (cin or K) * (cout or N) * M * batch
+    if GEMM_X3 and K >= GEMM_X3_MINK and K % 32 == 0 and N % 128 == 0 and lda % 4 == 0 and ldo % 4 == 0 and a_off % 4 == 0 \
+            and (res is None or ldr % 4 == 0):
+        # own split-bf16 GEMM (gemm_x3.hip): 6 bf16 term products per f32 product
+        w3 = ops.gemm_weights_x3(w)
+        plan.buffers.append([w3, bias])
+        plan.add("krrn_gemm_x3_f32", P(a.data_ptr() + 4 * a_off), lda, M, K, N, ptr(w3), ptr(bias), ptr(res), ldr,
+                 ptr(out), ldo, int(relu), batch, a_grp, o_grp, r_grp,
+                 meta=dict(kernel="gemm_x3", flops=flops, tag=tag, M=M * batch, N=N, K=K, splits=1,
+                           mfma_flops=2.0 * M * batch * N * K * 6 / 16, mfma_bf16_flops=2.0 * M * batch * N * K * 6))
+        return True
     h = ctypes.c_void_p()
     wsb = ctypes.c_longlong()
     st = _lib.lib().krrn_blas_gemm_create(M, N, K, lda, ldo, batch, a_grp, o_grp, int(bias is not None), int(relu),

@@ -73,6 +73,14 @@ for shp in shapes:
     line.append(f"LT {ms*1e3:.1f}us {fl/ms/1e9:.0f}TF ws={wsb.value}" + (" ERR" if err > 1e-5 else "") +
                 ("" if torch.equal(o1, out) else " NONDET"))
     _lib.lib().krrn_blas_gemm_destroy(h)
+    w3f = ops.gemm_weights_x3(W)
+    out = torch.zeros(M, N, device=dev)
+    fn = lambda: _lib.check(_lib.lib().krrn_gemm_x3_f32(ptr(A), a_cs, M, K, N, ptr(w3f), ptr(bias), ptr(None), 0,  # noqa: E731
+                                                        ptr(out), N, 0, 1, 0, 0, 0, st), "gemm_x3")
+    if K % 32 == 0 and N % 128 == 0:
+        ms = ev_time(fn)
+        err = float((out - ref).abs().max() / ref.abs().max())
+        line.append(f"GX3 {ms*1e3:.1f}us {fl/ms/1e9:.0f}TF" + (" ERR" if err > 1e-5 else ""))
     Ac = A[:, :K].contiguous()
     Wt = W.t().contiguous()
     ms = ev_time(lambda: torch.mm(Ac, Wt))
