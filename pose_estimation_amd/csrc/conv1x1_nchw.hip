@@ -14,7 +14,8 @@
 
 namespace {
 
-constexpr int kPx = 64;  // pixels per block (16 per wave)
+constexpr int kPx = 64;       // pixels per block (16 per wave)
+constexpr int kOP = kPx + 4;  // output staging pitch (floats)
 
 // Persistent blocks: the weights are staged once per block, then the block walks its 64-pixel
 // tiles (b, px0), the next tile's pixel rows loaded into registers while the current tile's
@@ -24,7 +25,7 @@ __global__ __launch_bounds__(256) void conv1x1_nchw_kernel(const float* __restri
                                                            int HW, int K, int Kp, const float* __restrict__ wt, int N,
                                                            int n_store, const float* __restrict__ scale,
                                                            const float* __restrict__ bias, float* __restrict__ out,
-                                                           int out_cs, int out_co) {
+                                                           int out_cs, int out_co, int vec) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int pitch = Kp + 4;  // odd number of 16-B slots per row: conflict-free b128 reads
   float* sx = lds;                  // [kPx][pitch]
@@ -85,7 +86,30 @@ __global__ __launch_bounds__(256) void conv1x1_nchw_kernel(const float* __restri
       }
     }
     // acc[t][i] = (channel 16 t + 4 g + i, pixel 16 wave + fr)
-    const int b = tile / tpi, px = (tile - b * tpi) * kPx + 16 * wave + fr;
+    const int b = tile / tpi, px0 = (tile - b * tpi) * kPx;
+    if (vec) {
+      // transposed through LDS (sx is free once every wave's MFMAs are done): each channel's 64
+      // pixels leave as one 256-B run of float4 stores instead of four 64-B lane-group runs
+      __syncthreads();
+      float* so = sx;  // [16 NT][kOP]
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) so[(16 * t + 4 * g + i) * kOP + 16 * wave + fr] = acc[t][i];
+      __syncthreads();
+      float* ob = out + ((long long)b * out_cs + out_co) * HW + px0;
+      for (int e = tid; e < n_store * (kPx / 4); e += 256) {
+        const int n = e / (kPx / 4), q = e - n * (kPx / 4);
+        if (px0 + 4 * q >= HW) continue;  // HW % 4 == 0: a float4 is all in or all out
+        const float sc = scale ? scale[n] : 1.f, bi = bias ? bias[n] : 0.f;
+        f32x4 v = *reinterpret_cast<const f32x4*>(so + n * kOP + 4 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] * sc + bi;
+        *reinterpret_cast<f32x4*>(ob + (long long)n * HW + 4 * q) = v;
+      }
+      continue;
+    }
+    const int px = px0 + 16 * wave + fr;
     if (px < HW) {
       float* ob = out + ((long long)b * out_cs + out_co) * HW + px;
 #pragma unroll
@@ -118,6 +142,9 @@ KRRN_API int krrn_conv1x1_nchw_f32(const float* in, int in_cs, int in_co, int B,
   const int per_cu = (int)((160 * 1024) / lds);
   const dim3 grid(min(ntiles, 256 * (per_cu < 1 ? 1 : per_cu)));
   hipStream_t s = (hipStream_t)stream;
+  // float4 NCHW stores when every channel plane starts 16-B aligned and the staging tile
+  // (16 nt x kOP floats) fits the pixel-row region sx (kPx x (Kp + 4)): the heads' K = 128
+  const int vec = (HW % 4 == 0) && krrn_aligned16(out) && kPx * (Kp + 4) >= 16 * nt * kOP ? 1 : 0;
 #define KRRN_1X1(NTV)                                                                                                   \
   if (nt == NTV) {                                                                                                      \
     if (lds > 64 * 1024) {                                                                                              \
@@ -126,7 +153,7 @@ KRRN_API int krrn_conv1x1_nchw_f32(const float* in, int in_cs, int in_co, int B,
       if (e != hipSuccess) return (int)e;                                                                               \
     }                                                                                                                   \
     hipLaunchKernelGGL(conv1x1_nchw_kernel<NTV>, grid, dim3(256), lds, s, in, in_cs, in_co, B, HW, cin, Kp, wt, N,     \
-                       n_store, scale, bias, out, out_cs, out_co);                                                      \
+                       n_store, scale, bias, out, out_cs, out_co, vec);                                                 \
     return krrn_launch_status();                                                                                        \
   }
   KRRN_1X1(1) KRRN_1X1(2) KRRN_1X1(3) KRRN_1X1(4) KRRN_1X1(5)

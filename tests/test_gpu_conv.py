@@ -362,7 +362,8 @@ def test_conv_small_group(dev):
 
 
 @pytest.mark.parametrize("B,HW,cin,cout,co,oc,Cx", [(3, 1000, 128, 72, 0, 0, 72), (2, 777, 128, 3, 0, 0, 3),
-                                                   (4, 64, 20, 40, 4, 5, 50), (1, 130, 256, 80, 0, 0, 80)])
+                                                   (4, 64, 20, 40, 4, 5, 50), (1, 130, 256, 80, 0, 0, 80),
+                                                   (2, 1000, 128, 9, 0, 3, 12)])
 def test_conv1x1_nchw(dev, B, HW, cin, cout, co, oc, Cx):
     """krrn_conv1x1_nchw_f32 (the heads' final 1x1 convs) vs torch fp32: ragged pixel tiles, K not a
     multiple of 16, channel-offset input and output."""
