@@ -276,17 +276,27 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
   int yo[KU];
 #pragma unroll
   for (int j = 0; j < KU; ++j) yo[j] = (KC || j < kk) ? nbp[j] * yrow + C : 0;
+  // 3-D directions of a fixed neighbour count (level 0 / 1: 30 floats) live in registers for the
+  // whole point; the 9-D level-2 ones stay in LDS behind an opaque pointer (see below)
+  constexpr bool kHoist = KC > 0 && D * KU <= 48;
+  float dreg[kHoist ? KU * D : 1];
+  if constexpr (kHoist) {
+#pragma unroll
+    for (int e = 0; e < KU * D; ++e) dreg[e] = dp[e];
+  }
   for (int c = 4 * l; c < C; c += 4 * LP) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     // The support loop stays rolled and, where Y is gathered, the LDS direction reads stay
     // inside it (an opaque pointer per iteration): unrolled and hoisted into paired registers
     // they took every VGPR (level 2, 9-D: occupancy 1, 170 -> 70 us per launch). The surface
-    // conv (no gathers, VALU-bound) keeps its hoisted directions.
+    // conv (no gathers, VALU-bound) and the 3-D gathered convs (kHoist: 30 floats, occupancy 4 -> 2
+    // but no flat loads in the loop; all gather-convs 1.16 -> 1.10 ms per step) keep theirs in
+    // registers.
 #pragma unroll 1
     for (int s = 0; s < S; ++s) {
       const int so = s * C + c;
       const float* dps = dp;
-      if constexpr (HAS_Y) asm volatile("" : "+v"(dps));
+      if constexpr (HAS_Y && !kHoist) asm volatile("" : "+v"(dps));
       f32x4 yv[HAS_Y ? KU : 1];
       if constexpr (HAS_Y) {
 #pragma unroll
@@ -300,7 +310,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
 #pragma unroll
       for (int j = 0; j < KU; ++j) {
         if (!KC && j >= kk) break;
-        const float* dr = dps + j * D;
+        const float* dr = kHoist ? dreg + j * D : dps + j * D;
         f32x4 th = dr[0] * w[0];
 #pragma unroll
         for (int i = 1; i < D; ++i) th += dr[i] * w[i];
