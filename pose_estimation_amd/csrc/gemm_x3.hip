@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
   const float* abase = g.a + grp * g.a_grp + (size_t)m0 * g.lda;
   const int rows = min(BM, g.M - m0);
   const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, rows * g.lda * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, ((rows - 1) * g.lda + g.K) * 4, 0x00020000);
   unsigned aoff[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) aoff[i] = (unsigned)(((srow + 64 * i) * g.lda + kq) * 4);
@@ -93,11 +93,14 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
   const int G = g.K >> 3;  // 8-k groups
   const unsigned* wb = g.w + ((size_t)((n0 >> 5) + wave) * G) * 512 + lane * 4;
 
-  // every load is unconditional (no branches in the loop body, so the waitcnts stay exact):
-  // chunks past the last read zeros past the buffer or unused row data, weight groups past the
-  // last are clamped to it
+  // every load is unconditional (no branches in the loop body, so the waitcnts stay exact): the
+  // prefetches past the last chunk / weight group reload the last one (never used), so no read
+  // leaves the caller's rows: a row's k < K only, and the last row of a column-offset A (a_off
+  // + K <= lda) ends inside the tensor
+  const int nch = g.K / KC;  // even (K % 32 == 0)
   f32x4 ra[2][2];  // A chunks c + 1 and c + 2 in flight (2 float4 per thread per chunk)
   auto load_a = [&](int c, int s) {
+    c = min(c, nch - 1);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       ra[s][i] = __builtin_bit_cast(
@@ -157,7 +160,6 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
   //   phase 2: read group 0 of chunk c + 1 | MFMAs of group 1.
   // sched_barrier(0) pins the phases, so every LDS read is a whole group ahead of its MFMAs and
   // the split VALU hides under MFMAs instead of serialising with them.
-  const int nch = g.K / KC;  // even (K % 32 == 0)
   static_assert(NG == 2, "the chunk schedule below is written for 2 groups per chunk");
   Frag fa, fb;
   load_a(0, 0);
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
       __builtin_amdgcn_sched_barrier(0);
       load_w(gi + 2, (2 * h + 2) & 3);
       read_frag(h, 1, fb);
-      store_a(1 - h);  // chunk c + h + 1 (zeros / unused past the end)
+      store_a(1 - h);  // chunk c + h + 1 (a reloaded last chunk past the end: unused)
       mma(fa, 2 * h);
       __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);   // weight loads
       __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // DS reads

@@ -395,8 +395,9 @@ def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str 
 BLAS = os.environ.get("KRRN_BLAS", "1") == "1"
 BLAS_MAX_WS = 64 << 20
 # plain GEMMs with K >= GEMM_X3_MINK on gemm_x3.hip (split-bf16), the rest on hipBLASLt: measured
-# (profiles/bench_gemm.py, MI355X) 10-18 % faster at K = 256..1024, no faster at K = 128 (the
-# level-0/1 GCN GEMMs: output-write-bound, 262 MB per launch)
+# (profiles/bench_gemm.py, MI355X) 10-18 % faster at K = 256..1024, 10 % slower at K = 128 (the
+# level-0 GCN GEMMs: 198 vs 180 us, output-write-bound) and slower at layer1's K = 64 (all
+# eligible GEMMs on gemm_x3: 1.98 vs 1.77 ms of GEMMs per step)
 GEMM_X3 = os.environ.get("KRRN_GEMM_X3", "1") == "1"
 GEMM_X3_MINK = int(os.environ.get("KRRN_GEMM_X3_MINK", "256"))
 
