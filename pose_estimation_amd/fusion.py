@@ -250,4 +250,4 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
                      N * 1280, 1280, 384, B)
     plan.buffers.append(keep)
     return feat, dict(pool_v=nb4["v"], pool_x=nb4["x"], pool_n=nb4["n"], pool2=nb4b, idx0=idx0, idx1=idx1, idx2=idx2, nn1=nn1, nn2=nn2, feat1=feat1, feat2=feat2, fm5=fm5,
-                      F0=F0, V1=V1, PV1=PV1, PV2=PV2, FP1=FP1, FP2=FP2, fm4=fm4)
+                      F0=F0, V1=V1, PV1=PV1, PV2=PV2, FP1=FP1, FP2=FP2, fm4=fm4, Y1=Y1, Y2=Y2, Y4=Y4, Y5=Y5)
