@@ -1,0 +1,58 @@
+"""Out-of-bounds write detector for the plan kernels: every plan buffer gets a guard region filled
+with a byte pattern right after its end; after one step every guard must be intact. A kernel that
+writes past its output buffer shows up as the buffer (and the plan line that allocated it) whose
+guard changed. usage: python3 profiles/guard_check.py [B S N backbone]"""
+import os
+import sys
+import traceback
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pose_estimation_amd import KRRN, make_config, runtime  # noqa: E402
+from pose_estimation_amd.pipeline import BatchPipeline  # noqa: E402
+from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
+
+GUARD = 1 << 16  # bytes
+PAT = 0xA5
+records = []
+
+
+def guarded_buf(self, shape, dtype=torch.float32, zero=True):
+    n = 1
+    for s in shape:
+        n *= int(s)
+    es = torch.empty((), dtype=dtype).element_size()
+    raw = torch.empty(n * es + GUARD, dtype=torch.uint8, device=self.device)
+    if zero:
+        raw[:n * es].zero_()
+    raw[n * es:].fill_(PAT)
+    t = raw[:n * es].view(dtype).view(tuple(shape))
+    self.buffers.append(raw)
+    where = [f for f in traceback.extract_stack()[:-1] if "pose_estimation_amd" in f.filename][-2:]
+    records.append((raw, n * es, tuple(shape), dtype, "; ".join(f"{os.path.basename(f.filename)}:{f.lineno}"
+                                                                 for f in where)))
+    return t
+
+
+runtime.Plan.buf = guarded_buf
+B, S, N = (int(v) for v in sys.argv[1:4]) if len(sys.argv) > 3 else (4, 64, 256)
+bb = sys.argv[4] if len(sys.argv) > 4 else "w18"
+dev = torch.device("cuda", 0)
+m = KRRN(cfg=make_config(num_cls=1, backbone=bb))
+init_weights(m, 0)
+m = m.to(dev).eval()
+d = make_batch(B, S, N, seed=22)
+pl = BatchPipeline(m, B, S, N, dev, parts=1, seed=0)
+pl.load(d)
+pl.run()
+torch.cuda.synchronize()
+bad = 0
+for raw, nb, shape, dtype, where in records:
+    g = raw[nb:]
+    if not bool((g == PAT).all()):
+        idx = torch.nonzero(g != PAT).flatten()
+        bad += 1
+        print(f"OVERWRITTEN guard of {shape} {dtype} from {where}: {idx.numel()} bytes, first at +{int(idx[0])}, "
+              f"last at +{int(idx[-1])}", flush=True)
+print(f"B={B} S={S} N={N} {bb}: {len(records)} buffers checked, {bad} guards overwritten", flush=True)
