@@ -109,22 +109,21 @@ __global__ __launch_bounds__(kKnnThreads) void knn_kernel(
       const float d = mode == 0 ? ((inner * -2.f) + cn) + qn : (cn + qn) - 2.f * inner;
       if (d < bd[KS - 1]) {
         // insertion in front of the first strictly larger entry (candidates of one lane arrive
-        // in increasing index, so equal distances stay in index order); branch-free shift
+        // in increasing index, so equal distances stay in index order), branch-free from the old
+        // list: with c_s = d < bd[s] (monotone in s), slot s takes the old s - 1 entry where
+        // c_{s-1}, the new one where c_s only, else keeps its own; the distance of that choice is
+        // exactly med3(d, bd[s-1], bd[s]) (the list is sorted), one v_med3_f32 per slot
         const int ni = j0 + j;
-        bool ins = false;
-        float cd = 0.f;
-        int ci = 0;
+        bool c[KS];
 #pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-          const bool here = !ins && (d < bd[s2]);
-          const float od = bd[s2];
-          const int oi = bi[s2];
-          bd[s2] = ins ? cd : (here ? d : od);
-          bi[s2] = ins ? ci : (here ? ni : oi);
-          cd = od;
-          ci = oi;
-          ins = ins || here;
+        for (int s2 = 0; s2 < KS; ++s2) c[s2] = d < bd[s2];
+#pragma unroll
+        for (int s2 = KS - 1; s2 > 0; --s2) {
+          bi[s2] = c[s2 - 1] ? bi[s2 - 1] : (c[s2] ? ni : bi[s2]);
+          bd[s2] = __builtin_amdgcn_fmed3f(d, bd[s2 - 1], bd[s2]);
         }
+        bi[0] = c[0] ? ni : bi[0];
+        bd[0] = fminf(d, bd[0]);
       }
     }
   }
