@@ -289,6 +289,13 @@ int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choose, int N
 int krrn_randperm_i32(const unsigned long long* seed_ptr, unsigned int stream_id, int n, int k, int rows, int* out,
                       void* stream);
 
+/* Up to 8 independent single-row draws of krrn_randperm_i32 in ONE launch (the five Pool_layer
+ * permutations of a forward, gcn3d.py:239): draw q is torch.randperm(n[q])[:k[q]] for stream id
+ * stream_id[q] into out[q], bit-identical to krrn_randperm_i32(seed_ptr, stream_id[q], n[q], k[q],
+ * 1, out[q]); the draws run side by side (one block each) instead of back to back. */
+int krrn_randperm_multi_i32(const unsigned long long* seed_ptr, int count, const unsigned int* stream_id, const int* n,
+                            const int* k, int* const* out, void* stream);
+
 /* RANSAC subsets: 5 distinct indices in [0, P) per (crop, hypothesis); out int32 [B][H][5]. */
 int krrn_ransac_subsets(const unsigned long long* seed_ptr, unsigned int stream_id, int B, int H, int P, int* out,
                         void* stream);

@@ -28,11 +28,8 @@ __device__ __forceinline__ unsigned int rand32(unsigned long long seed, unsigned
 
 constexpr int kPermMax = 4096;
 
-__global__ __launch_bounds__(1024) void randperm_kernel(const unsigned long long* __restrict__ seed_ptr,
-                                                        unsigned int stream, int n, int k, int* __restrict__ out) {
-  __shared__ unsigned long long keys[kPermMax];
-  const int row = blockIdx.x;
-  const unsigned long long seed = *seed_ptr;
+__device__ __forceinline__ void randperm_row(unsigned long long* keys, unsigned long long seed, unsigned int stream,
+                                             int row, int n, int k, int* __restrict__ out) {
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
   for (int i = threadIdx.x; i < np2; i += blockDim.x) {
@@ -53,6 +50,26 @@ __global__ __launch_bounds__(1024) void randperm_kernel(const unsigned long long
     }
   }
   for (int i = threadIdx.x; i < k; i += blockDim.x) out[(long long)row * k + i] = (int)(keys[i] & 0xffffffffu);
+}
+
+__global__ __launch_bounds__(1024) void randperm_kernel(const unsigned long long* __restrict__ seed_ptr,
+                                                        unsigned int stream, int n, int k, int* __restrict__ out) {
+  __shared__ unsigned long long keys[kPermMax];
+  randperm_row(keys, *seed_ptr, stream, blockIdx.x, n, k, out);
+}
+
+constexpr int kMultiMax = 8;
+struct PermDraws {
+  unsigned int stream[kMultiMax];
+  int n[kMultiMax], k[kMultiMax];
+  int* out[kMultiMax];
+};
+
+__global__ __launch_bounds__(1024) void randperm_multi_kernel(const unsigned long long* __restrict__ seed_ptr,
+                                                              const PermDraws d) {
+  __shared__ unsigned long long keys[kPermMax];
+  const int q = blockIdx.x;
+  randperm_row(keys, *seed_ptr, d.stream[q], 0, d.n[q], d.k[q], d.out[q]);
 }
 
 __global__ void subsets_kernel(const unsigned long long* __restrict__ seed_ptr, unsigned int stream, int H, int P,
@@ -82,6 +99,20 @@ KRRN_API int krrn_randperm_i32(const unsigned long long* seed_ptr, unsigned int 
   if (!seed_ptr || !out) return KRRN_EARG;
   if (n < 1 || n > kPermMax || k < 1 || k > n || rows < 1) return KRRN_ESHAPE;
   hipLaunchKernelGGL(randperm_kernel, dim3(rows), dim3(1024), 0, (hipStream_t)hstream, seed_ptr, stream, n, k, out);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_randperm_multi_i32(const unsigned long long* seed_ptr, int count, const unsigned int* stream_id,
+                                     const int* n, const int* k, int* const* out, void* hstream) {
+  if (!seed_ptr || !stream_id || !n || !k || !out) return KRRN_EARG;
+  if (count < 1 || count > kMultiMax) return KRRN_ESHAPE;
+  PermDraws d;
+  for (int q = 0; q < count; ++q) {
+    if (!out[q]) return KRRN_EARG;
+    if (n[q] < 1 || n[q] > kPermMax || k[q] < 1 || k[q] > n[q]) return KRRN_ESHAPE;
+    d.stream[q] = stream_id[q]; d.n[q] = n[q]; d.k[q] = k[q]; d.out[q] = out[q];
+  }
+  hipLaunchKernelGGL(randperm_multi_kernel, dim3(count), dim3(1024), 0, (hipStream_t)hstream, seed_ptr, d);
   return krrn_launch_status();
 }
 

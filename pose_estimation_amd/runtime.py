@@ -40,6 +40,7 @@ _lib.register("krrn_gather2_add_f32", [P, P, L, I, P, P, L, I, I, I, P, P, P, I,
 _lib.register("krrn_pnp_ransac_f32", [P, I, P, I, P, I, P, P, P, P, P, P, I, F, F, P, P, P, P, P, I, P])
 _lib.register("krrn_randperm_i32", [P, U, I, I, I, P, P])
 _lib.register("krrn_ransac_subsets", [P, U, I, I, I, P, P])
+_lib.register("krrn_randperm_multi_i32", [P, I, P, P, P, P, P])
 _lib.register("krrn_rng_advance", [P, P])
 _lib.register("krrn_conv2d_group_f32", [P, I, I, P])
 _lib.register("krrn_conv2d_group_x3_f32", [P, I, I, P])

@@ -157,3 +157,32 @@ def test_device_rng(dev):
     assert all(len(set(row.tolist())) == 5 for row in s)
     assert s.min() >= 0 and s.max() < 256
 
+
+
+def test_device_rng_multi_matches_single(dev):
+    """krrn_randperm_multi_i32 (the five pool permutations in one launch) equals the five
+    krrn_randperm_i32 single-row launches draw for draw."""
+    import ctypes
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import ptr, P
+    seed = torch.tensor([987654321], dtype=torch.int64, device=dev)
+    st = P(torch.cuda.current_stream().cuda_stream)
+    draws = [(0, 1000, 250), (1, 1000, 250), (2, 1000, 250), (3, 1000, 250), (4, 250, 62), (7, 4096, 1)]
+    singles = []
+    for sid, n, k in draws:
+        o = torch.empty(k, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().krrn_randperm_i32(ptr(seed), sid, n, k, 1, ptr(o), st), "randperm")
+        singles.append(o)
+    multi = [torch.full((k,), -1, dtype=torch.int32, device=dev) for _, _, k in draws]
+    c = len(draws)
+    sids = (ctypes.c_uint * c)(*[d[0] for d in draws])
+    ns = (ctypes.c_int * c)(*[d[1] for d in draws])
+    ks = (ctypes.c_int * c)(*[d[2] for d in draws])
+    outs = (ctypes.c_void_p * c)(*[m.data_ptr() for m in multi])
+    _lib.check(_lib.lib().krrn_randperm_multi_i32(ptr(seed), c, sids, ns, ks, outs, st), "randperm multi")
+    torch.cuda.synchronize()
+    for a, b in zip(singles, multi):
+        assert torch.equal(a, b)
+    bad = (ctypes.c_int * c)(*([5000] * c))
+    assert _lib.lib().krrn_randperm_multi_i32(ptr(seed), c, sids, bad, ks, outs, st) < 0
+    assert _lib.lib().krrn_randperm_multi_i32(ptr(seed), 9, sids, ns, ks, outs, st) < 0
