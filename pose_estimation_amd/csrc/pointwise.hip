@@ -225,22 +225,25 @@ __global__ void gather_rows_kernel(const void* __restrict__ idx, long long idx_b
 
 // pred_t[b] = mean_i( cloud[b, i] + W4[0:3] . h[b, i] + b4[0:3] )   (one block per crop)
 // TBase conv4 (C -> 3, +bias) and pred_t = mean_N(cloud + t_res) (posenet.py:80, krrn.py:150-153).
-// One block per crop; 4 lanes per point, each lane a float4 stripe of the C-channel row (a wave
-// reads 16 rows x 64 contiguous bytes per load), 2 shuffles finish the dot product. The mean is a
-// fixed-order reduction (per-lane partials, then a fixed tree), so runs are bit-reproducible.
-__global__ __launch_bounds__(256) void tbase_tail_kernel(const float* __restrict__ h, int n, int C,
+// One block of 16 waves per crop (the B = 64 blocks cannot fill the chip, so each brings 256 points
+// into flight per pass: 77 -> ~25 us per launch); 4 lanes per point, each lane a float4 stripe of the
+// C-channel row (a wave reads 16 rows x 64 contiguous bytes per load), 2 shuffles finish the dot
+// product. The mean is a fixed-order reduction (per-lane partials, then a fixed tree), so runs are
+// bit-reproducible.
+constexpr int kTailWaves = 16;
+__global__ __launch_bounds__(64 * kTailWaves) void tbase_tail_kernel(const float* __restrict__ h, int n, int C,
                                                          const float* __restrict__ w4,
                                                          const float* __restrict__ b4,
                                                          const float* __restrict__ cloud,
                                                          float* __restrict__ pred_t, float* __restrict__ t_res) {
-  __shared__ float red[4][3];
+  __shared__ float red[kTailWaves][3];
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = lane & 3, pl = lane >> 2;
   const int C4 = C >> 2;
   const float bx = b4[0], by = b4[1], bz = b4[2];
   float sx = 0.f, sy = 0.f, sz = 0.f;
-  for (int i0 = 0; i0 < n; i0 += 64) {
+  for (int i0 = 0; i0 < n; i0 += 16 * kTailWaves) {
     const int i = i0 + wave * 16 + pl;
     if (i < n) {
       const f32x4* hr = reinterpret_cast<const f32x4*>(h + ((long long)b * n + i) * C);
@@ -285,7 +288,10 @@ __global__ __launch_bounds__(256) void tbase_tail_kernel(const float* __restrict
   __syncthreads();
   if (threadIdx.x < 3) {
     const int j = threadIdx.x;
-    pred_t[b * 3 + j] = (red[0][j] + red[1][j] + red[2][j] + red[3][j]) / (float)n;
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < kTailWaves; ++w) acc += red[w][j];
+    pred_t[b * 3 + j] = acc / (float)n;
   }
 }
 
@@ -438,7 +444,7 @@ KRRN_API int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const floa
   if (!h || !w4 || !b4 || !cloud || !pred_t) return KRRN_EARG;
   if (B < 1 || n < 1 || C < 1) return KRRN_ESHAPE;
   if ((C & 3) || !krrn_aligned16(h) || !krrn_aligned16(w4)) return KRRN_EALIGN;
-  hipLaunchKernelGGL(tbase_tail_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, h, n, C, w4, b4, cloud, pred_t,
+  hipLaunchKernelGGL(tbase_tail_kernel, dim3(B), dim3(64 * kTailWaves), 0, (hipStream_t)stream, h, n, C, w4, b4, cloud, pred_t,
                      t_res);
   return krrn_launch_status();
 }
