@@ -202,6 +202,8 @@ def _cpu_config(B: int, S: int, N: int, backbone: str, warmup: int, reps: int, s
         print(f"[cpu leg] B={B} {backbone} iter {i}: {el:.2f} s", file=sys.stderr, flush=True)
         if i >= warmup:
             times.append(el)
+    if not times:
+        return {"value": None, "batch": B, "backbone": f"hrnet_{backbone}", "warmup": warmup, "reps": 0}
     med = statistics.median(times)
     return {"value": round(B / med, 4), "batch": B, "backbone": f"hrnet_{backbone}", "warmup": warmup, "reps": reps,
             "median_s_per_batch": round(med, 4)}
@@ -210,8 +212,8 @@ def _cpu_config(B: int, S: int, N: int, backbone: str, warmup: int, reps: int, s
 def cpu_baseline(S: int, N: int, threads: int, reps2: int, warmup2: int):
     """the CPU oracle on the GPU box's host cores, config 1 (B = 1, the reference's
     HRNet config.yaml widths) and config 2 (B = 64, HRNet-W18), S = 120, N = 1000, crops/s as the
-    median of timed batches after warm-ups (config 1: 3 + 10; config 2: `warmup2` + `reps2`, 1 + 3
-    by default to bound the run — `--cpu-reps 10 --cpu-warmup 3` gives the full protocol)."""
+    median of timed batches after warm-ups (config 1: 3 + 10; config 2: `warmup2` + `reps2`, the
+    protocol's 3 + 10 by default, ~3 minutes on the GPU box's 16-CPU quota)."""
     torch.set_num_threads(threads)
     c1 = _cpu_config(1, S, N, "lm", 3, 10, 0)
     c2 = _cpu_config(64, S, N, "w18", warmup2, reps2, 0)
@@ -272,6 +274,111 @@ def cpu_leg_accuracy(dev, B: int = 64, N: int = 1000, S: int = 120, seed: int = 
                       "ADD-S for half the crops; AUC max_dis 0.1 m (metric.py:38-65)"}
 
 
+def config3_sizes(total: int, seed: int = 0):
+    """BASELINE config 3's crop sizes: `total` crops with S drawn from the LineMOD test-crop
+    histogram (13,425 yolov3 detections snapped by get_square_bbox, batchdataset.py:890-923)."""
+    import numpy as np
+    from pose_estimation_amd.dataset import LM_CROP_HIST
+    hs = np.array(list(LM_CROP_HIST.keys()))
+    hp = np.array(list(LM_CROP_HIST.values()), dtype=np.float64)
+    return [int(v) for v in np.random.default_rng(seed).choice(hs, size=total, p=hp / hp.sum())]
+
+
+def _config3_cap(buckets: dict, world: int) -> int:
+    """Rows of a rank's per-step record block: the most crops any rank holds per bucket, summed (the
+    same on every rank, as all_gather_into_tensor needs; shorter ranks leave zero rows)."""
+    return max(1, sum(max(kd.shard_range(n, world, r)[1] - kd.shard_range(n, world, r)[0] for r in range(world))
+                      for n in buckets.values()))
+
+
+def bench_config3(args, rank: int, world: int, local: int):
+    """BASELINE config 3: all 13 LineMOD objects, one global batch of args.global_batch crops per step
+    with crop sizes from the LineMOD histogram. Like trainer.py:521-551 (process_patch_datas) and the
+    eval batcher (dataset.BucketBatcher), crops are bucketed by S; every bucket is split contiguously
+    across the ranks (distributed.bucket_shard), each rank runs one captured BatchPipeline per bucket
+    it holds (forward + PnP on the GPU), and the per-crop pose records of the step are all-gathered
+    over RCCL. value = global crops / max-over-ranks step time (strong scaling)."""
+    from pose_estimation_amd.config import LM_OBJLIST
+    N = args.points
+    sizes = config3_sizes(args.global_batch)
+    shard = kd.bucket_shard(sizes, world, rank)
+    buckets_all = {S: sizes.count(S) for S in sorted(set(sizes))}
+    if args.dry_run:
+        dev = torch.device("cpu")
+        pipes = []
+        record = torch.zeros((_config3_cap(buckets_all, world), kd.RECORD), dtype=torch.float32)
+        one_step = lambda: _dry_step(record.shape[0], world, record)  # noqa: E731
+        sync = lambda: None  # noqa: E731
+    else:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        model = KRRN(cfg=make_config(num_cls=13, backbone=args.backbone))
+        init_weights(model, 0)
+        model = model.to(dev).eval()
+        pipes = []
+        for S, idx in shard.items():
+            pl = BatchPipeline(model, len(idx), S, N, dev, parts=1, seed=rank * 97 + S)
+            pl.load(make_batch(len(idx), S, N, seed=1000 * rank + S, objlist=LM_OBJLIST))
+            pl.run()
+            torch.cuda.synchronize()
+            pl.capture()
+            pipes.append(pl)
+        record = torch.zeros((_config3_cap(buckets_all, world), kd.RECORD), dtype=torch.float32, device=dev)
+
+        def one_step():
+            for pl in pipes:
+                pl.step()
+            if world > 1:
+                o = 0
+                for pl in pipes:
+                    r = pl.results()
+                    b = r["R"].shape[0]
+                    kd.pack_records(r["R"], r["t"], r["pred_t"], r["inliers"], out=record[o:o + b])
+                    o += b
+                kd.gather_records(record)
+        sync = torch.cuda.synchronize
+    for _ in range(args.warmup):
+        one_step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev if not args.dry_run else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms = el / args.steps * 1e3
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(args.global_batch * args.steps / el, 2), "unit": "crops/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "dry run (no GPU)" if args.dry_run else
+                    "synthetic (seeded LineMOD-shaped crops of the 13 objects, random-init weights)",
+            "config": {"workload": f"BASELINE config 3: LineMOD all 13 objects, global batch {args.global_batch} "
+                                   f"crops (S from the LineMOD test-crop histogram, bucketed by S, every bucket "
+                                   f"split over {world} rank(s)), HRNet-{args.backbone.upper()} + {N}-pt fusion + "
+                                   f"TBase, PnP-RANSAC (H=100) on GPU",
+                       "global_batch": args.global_batch, "points": N, "buckets": buckets_all,
+                       "rank0_buckets": {S: len(v) for S, v in shard.items()},
+                       "backbone": f"hrnet_{args.backbone}", "classes": 13,
+                       "parallelism": f"dp{world}" if world > 1 else "single", "graph": not args.dry_run},
+            "roofline": None, "cpu_baseline": None,
+        }
+        if args.dry_run:
+            line["dry_run"] = True
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def launch_ranks(n: int) -> int:
     """`--gpus N` without a launcher: start N rank processes (this script, RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* set, one GPU each) and wait. The parent never touches the GPU, and the
@@ -320,14 +427,20 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU leg (baseline + accuracy)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="torch threads of the CPU leg (0 = the CPUs this process may use: cgroup quota / affinity)")
-    ap.add_argument("--cpu-reps", type=int, default=3, help="timed B=64 CPU batches (BASELINE.md §2 protocol: 10)")
-    ap.add_argument("--cpu-warmup", type=int, default=1, help="untimed B=64 CPU batches (protocol: 3)")
+    ap.add_argument("--cpu-reps", type=int, default=10, help="timed B=64 CPU batches (BASELINE.md §2 protocol: 10)")
+    ap.add_argument("--cpu-warmup", type=int, default=3, help="untimed B=64 CPU batches (protocol: 3)")
     ap.add_argument("--breakdown", default="", help="write the per-kernel breakdown JSON here")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks, a host-delay step and the record all-gather (launcher rehearsal)")
     ap.add_argument("--micro", type=int, default=1,
                     help="micro-batches processed concurrently inside each step (pipeline.py)")
     ap.add_argument("--flat", action="store_true", help="no plan side streams inside a micro-batch")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3],
+                    help="BASELINE config: 2 = LineMOD 'cat', B crops per GPU (default; weak scaling); 3 = all 13 "
+                         "LineMOD objects, ONE global batch of --global-batch crops whose sizes S are drawn from the "
+                         "LineMOD test-crop histogram, bucketed by S and every bucket split across the ranks "
+                         "(distributed.bucket_shard; strong scaling: the 256 crops are shared by the N GPUs)")
+    ap.add_argument("--global-batch", type=int, default=256, help="config 3: crops per step over all ranks")
     ap.add_argument("--pipeline", choices=["none", "backbone", "heads", "pose"], default="heads",
                     help="two-stage pipeline (pipeline.PipelinedPipeline) split after the backbone, the heads "
                          "(default: 16.0-16.3 vs 16.3-16.5 ms/step) or before get_pose: stage A of batch k+1 runs "
@@ -340,6 +453,8 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
 
     rank, world, local = kd.init_from_env("gloo" if args.dry_run else "nccl")
+    if args.config == 3:
+        return bench_config3(args, rank, world, local)
     B, S, N = args.batch, args.size, args.points
     C = args.classes
     frame = tuple(int(v) for v in args.frame.split("x"))

@@ -126,6 +126,17 @@ int krrn_gemm_x3_f32(const float* a, int lda, int M, int K, int N, const void* w
                      const float* res, int ldr, float* out, int ldo, int relu, int batch, long long a_grp,
                      long long o_grp, long long r_grp, void* stream);
 
+/* Short-K GEMM streaming its output (gemm_panel.hip): the fusion's level-0 / level-1 GCN
+ * `feature_map @ weights + bias` of Conv_layer (lib/network/point/gcn3d.py:136-164, K = 128,
+ * N = 8 * 128) and layer1's 64 -> 256 1x1 convs (myhrnet.py:65-103, K = 64):
+ *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n][k] + bias[n] + res[m*ldr + n]),  0 <= n < N
+ * Split-bf16 operands at f32 accuracy; each wave keeps its 32 activation rows in registers and
+ * walks 32-column tiles. wpf holds W split into per-wave fragments (ops.gemm_weights_panel:
+ * [N/32][K/8][3][64 lanes][4] u32). K = 64 or 128, N % 32 == 0, lda % 4 == 0, A / wpf 16-byte
+ * aligned; `csplit` column ranges per row panel (grid = ceil(M / 128) x csplit). */
+int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N, const void* wpf, const float* bias,
+                           const float* res, int ldr, float* out, int ldo, int relu, int csplit, void* stream);
+
 /* 1x1 conv with NCHW output (the heads' final xyz / normal convs, lib/network/krrn.py:97-98,
  * 80-84): out[b][out_co + n][p] = scale[n] * sum_c in[(b * HW + p) * in_cs + in_co + c] wt[n][c]
  * + bias[n] for n < n_store, p < HW; out has out_cs channels per image. cin <= 256 (multiple of 4),
@@ -281,7 +292,7 @@ int krrn_tbase_tail_f32(const float* h, int B, int n, int C, const float* w4, co
  * the selection + EPnP on all inliers. */
 int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choose, int N, const int* sel, int P,
                         const float* xmap, const float* ymap, const float* K4, const double* extent,
-                        const double* lfborder, const int* subsets, int H, float thr, float conf, float* workspace,
+                        const double* lfborder, const int* subsets, int H, float thr, double conf, float* workspace,
                         float* R, float* t, int* inliers, unsigned char* inlier_mask, int B, void* stream);
 
 /* torch.randperm(n)[:k] per row (gcn3d.py:239, trainer.py:407) from a counter-based generator

@@ -26,7 +26,7 @@ def _load():
         _lib.oracle_epnp.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int] + [ctypes.c_void_p] * 3
         _lib.oracle_pnp_ransac.restype = ctypes.c_int
         _lib.oracle_pnp_ransac.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
-                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 

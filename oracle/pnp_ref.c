@@ -36,7 +36,7 @@
 static void jacobi_eig(double* A, int n, double* w, double* V) {
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0; /* columns = eigvecs during sweep */
-  for (int sweep = 0; sweep < 60; ++sweep) {
+  for (int sweep = 0; sweep < 40; ++sweep) {
     double off = 0.0, tot = 0.0;
     for (int p = 0; p < n; ++p)
       for (int q = 0; q < n; ++q) {
@@ -185,28 +185,55 @@ static int ransac_update_niters(double conf, double ep, int model_points, int ma
   return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
 }
 
-/* least squares min ||A x - b|| for A m x n (m <= 6, n <= 5) via the pseudo-inverse built
- * from the eigen-decomposition of A^T A (SVD: A^T A = V S^2 V^T). */
+/* least squares min ||A x - b|| for A m x n (m <= 6, n <= 5), as csrc/pnp.hip (lsq_rows) evaluates
+ * it: the normal equations summed row by row in order, Cholesky when A has full column rank (the
+ * usual case), else the pseudo-inverse from the eigen-decomposition of A^T A (OpenCV solves these
+ * with CV_SVD; the two agree to rounding on full-rank systems). */
 static void lsq_solve(const double* A, int m, int n, const double* b, double* x) {
-  double AtA[25], w[5], V[25], Atb[5];
-  for (int i = 0; i < n; ++i) {
-    for (int j = 0; j < n; ++j) {
-      double s = 0.0;
-      for (int k = 0; k < m; ++k) s += A[k * n + i] * A[k * n + j];
-      AtA[i * n + j] = s;
+  double AtA[25], w[5], V[25], Atb[5], C[25];
+  for (int i = 0; i < n * n; ++i) AtA[i] = 0.0;
+  for (int i = 0; i < n; ++i) Atb[i] = 0.0;
+  for (int k = 0; k < m; ++k)
+    for (int i = 0; i < n; ++i) {
+      for (int j = 0; j < n; ++j) AtA[i * n + j] += A[k * n + i] * A[k * n + j];
+      Atb[i] += A[k * n + i] * b[k];
     }
-    double s = 0.0;
-    for (int k = 0; k < m; ++k) s += A[k * n + i] * b[k];
-    Atb[i] = s;
+  double dmax = 0.0;
+  for (int i = 0; i < n; ++i) dmax = fmax(dmax, AtA[i * n + i]);
+  int spd = dmax > 0.0;
+  for (int j = 0; j < n; ++j) {
+    double d = AtA[j * n + j];
+    for (int k = 0; k < j; ++k) d -= C[j * n + k] * C[j * n + k];
+    spd = spd && d > 1e-14 * dmax;
+    const double cjj = sqrt(fmax(d, 1e-300));
+    C[j * n + j] = cjj;
+    for (int i = j + 1; i < n; ++i) {
+      double s = AtA[i * n + j];
+      for (int k = 0; k < j; ++k) s -= C[i * n + k] * C[j * n + k];
+      C[i * n + j] = s / cjj;
+    }
+  }
+  if (spd) {
+    double y[5];
+    for (int i = 0; i < n; ++i) {
+      double s = Atb[i];
+      for (int k = 0; k < i; ++k) s -= C[i * n + k] * y[k];
+      y[i] = s / C[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double s = y[i];
+      for (int k = i + 1; k < n; ++k) s -= C[k * n + i] * x[k];
+      x[i] = s / C[i * n + i];
+    }
+    return;
   }
   jacobi_eig(AtA, n, w, V);
   const double tol = (w[0] > 0 ? w[0] : 0.0) * 1e-24;
   for (int j = 0; j < n; ++j) x[j] = 0.0;
   for (int i = 0; i < n; ++i) {
-    if (w[i] <= tol) continue;
     double proj = 0.0;
     for (int k = 0; k < n; ++k) proj += V[i * n + k] * Atb[k];
-    proj /= w[i];
+    proj = (w[i] > tol) ? proj / w[i] : 0.0;
     for (int k = 0; k < n; ++k) x[k] += proj * V[i * n + k];
   }
 }
@@ -223,24 +250,47 @@ static void pinv3(const double* a, double* r) {
   const double tol = (w[0] > 0 ? w[0] : 0.0) * 1e-20;
   double P[9] = {0};
   for (int k = 0; k < 3; ++k) {
-    if (w[k] <= tol) continue;
+    const double iw = (w[k] > tol) ? 1.0 / w[k] : 0.0;
     for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) P[i * 3 + j] += V[k * 3 + i] * V[k * 3 + j] / w[k];
+      for (int j = 0; j < 3; ++j) P[i * 3 + j] += V[k * 3 + i] * V[k * 3 + j] * iw;
   }
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) r[i * 3 + j] = P[i * 3 + 0] * a[j * 3 + 0] + P[i * 3 + 1] * a[j * 3 + 1] + P[i * 3 + 2] * a[j * 3 + 2];
 }
 
-/* Procrustes: R, t minimising sum ||R pw + t - pc||^2 (Kabsch). */
-static void procrustes(const double* pw, const double* pc, int n, double* R, double* t) {
-  double cw[3] = {0, 0, 0}, cc[3] = {0, 0, 0};
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < 3; ++j) { cw[j] += pw[3 * i + j]; cc[j] += pc[3 * i + j]; }
-  for (int j = 0; j < 3; ++j) { cw[j] /= n; cc[j] /= n; }
-  double H[9] = {0}; /* H = sum (pc - cc)(pw - cw)^T   (ABt in EPnP) */
-  for (int i = 0; i < n; ++i)
-    for (int r = 0; r < 3; ++r)
-      for (int c = 0; c < 3; ++c) H[r * 3 + c] += (pc[3 * i + r] - cc[r]) * (pw[3 * i + c] - cw[c]);
+/* ---------------- the kernel's summation orders ---------------- */
+
+/* csrc/pnp.hip sums over points in one of two orders: SUM_SEQ, the points in order (a RANSAC
+ * hypothesis' 5 points, replicated in its 16-lane group: HypSum), or SUM_WAVE, the refinement on
+ * all inliers by one 64-lane wave (WaveSum): lane l sums points l, l + 64, ... in order, then the
+ * lanes combine by the butterfly v += shfl_xor(v, off), off = 32, 16, ..., 1 (lane 0's value).
+ * The rows of M^T M in SUM_WAVE: group g = lane / 16 sums points g, g + 4, ... in order, then
+ * (G0 + G1) + (G2 + G3). */
+enum { SUM_SEQ = 0, SUM_WAVE = 1 };
+static double contrib_buf[MAXP * 12];
+
+/* out[k] = sum over points of contrib[p * nv + k], in the kernel's order */
+static void reduce_points(int mode, int n, int nv, const double* contrib, double* out) {
+  for (int k = 0; k < nv; ++k) {
+    if (mode == SUM_SEQ) {
+      double v = 0.0;
+      for (int p = 0; p < n; ++p) v += contrib[p * nv + k];
+      out[k] = v;
+      continue;
+    }
+    double v[64], t[64];
+    for (int l = 0; l < 64; ++l) v[l] = 0.0;
+    for (int p = 0; p < n; ++p) v[p % 64] += contrib[p * nv + k];
+    for (int off = 32; off > 0; off >>= 1) {
+      for (int l = 0; l < 64; ++l) t[l] = v[l] + v[l ^ off];
+      for (int l = 0; l < 64; ++l) v[l] = t[l];
+    }
+    out[k] = v[0];
+  }
+}
+
+/* Kabsch on the 3x3 correlation H (csrc/pnp.hip kabsch): R = U diag(1,1,det) V^T. */
+static void kabsch(const double* H, double* R) {
   /* SVD H = U S V^T through eig(H^T H) = V S^2 V^T, U = H V / S */
   double HtH[9], w[3], V[9];
   for (int i = 0; i < 3; ++i)
@@ -275,7 +325,6 @@ static void procrustes(const double* pw, const double* pc, int n, double* R, dou
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 3; ++c)
       R[r * 3 + c] = U[0 * 3 + r] * V[0 * 3 + c] + U[1 * 3 + r] * V[1 * 3 + c] + U[2 * 3 + r] * v2[c];
-  for (int r = 0; r < 3; ++r) t[r] = cc[r] - (R[r * 3 + 0] * cw[0] + R[r * 3 + 1] * cw[1] + R[r * 3 + 2] * cw[2]);
 }
 
 /* ---------------- EPnP ---------------- */
@@ -284,21 +333,26 @@ typedef struct {
   double fu, fv, uc, vc;
 } Cam;
 
-static void ctrl_points(const double* pw, int n, double cws[4][3], double ccinv[9]) {
-  double c0[3] = {0, 0, 0};
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < 3; ++j) c0[j] += pw[3 * i + j];
-  for (int j = 0; j < 3; ++j) c0[j] /= n;
-  double C[9] = {0};
-  for (int i = 0; i < n; ++i)
-    for (int r = 0; r < 3; ++r)
-      for (int c = 0; c < 3; ++c) C[r * 3 + c] += (pw[3 * i + r] - c0[r]) * (pw[3 * i + c] - c0[c]);
+/* control points (PCA of the world points) and the inverse of their frame; cw = the centroid */
+static void ctrl_points(int mode, const double* pw, int n, double cws[4][3], double ccinv[9], double cw[3]) {
+  for (int p = 0; p < n; ++p)
+    for (int j = 0; j < 3; ++j) contrib_buf[3 * p + j] = pw[3 * p + j];
+  reduce_points(mode, n, 3, contrib_buf, cw);
+  for (int j = 0; j < 3; ++j) cw[j] /= n;
+  double C6[6];
+  for (int p = 0; p < n; ++p) {
+    const double d0 = pw[3 * p] - cw[0], d1 = pw[3 * p + 1] - cw[1], d2 = pw[3 * p + 2] - cw[2];
+    double* c = contrib_buf + 6 * p;
+    c[0] = d0 * d0; c[1] = d0 * d1; c[2] = d0 * d2; c[3] = d1 * d1; c[4] = d1 * d2; c[5] = d2 * d2;
+  }
+  reduce_points(mode, n, 6, contrib_buf, C6);
+  double C[9] = {C6[0], C6[1], C6[2], C6[1], C6[3], C6[4], C6[2], C6[4], C6[5]};
   double w[3], V[9];
   jacobi_eig(C, 3, w, V);
-  for (int j = 0; j < 3; ++j) cws[0][j] = c0[j];
+  for (int j = 0; j < 3; ++j) cws[0][j] = cw[j];
   for (int i = 0; i < 3; ++i) {
     const double k = sqrt((w[i] > 0 ? w[i] : 0.0) / n);
-    for (int j = 0; j < 3; ++j) cws[i + 1][j] = c0[j] + k * V[i * 3 + j];
+    for (int j = 0; j < 3; ++j) cws[i + 1][j] = cw[j] + k * V[i * 3 + j];
   }
   double CC[9];
   for (int i = 0; i < 3; ++i)
@@ -336,43 +390,59 @@ static void gauss_newton(const double* L, const double* rho, double betas[4]) {
   }
 }
 
-/* R,t from betas; returns mean reprojection error */
-static double r_and_t(const double* ut, const double betas[4], const double* pw, const double* uv, int n,
-                      double cws[4][3], const double* ci, Cam cam, double* R, double* t, double* pcs_buf) {
+/* R,t from betas (Procrustes on the camera-frame points, Kabsch); returns mean reprojection error */
+static double r_and_t(int mode, const double* ut, const double betas[4], const double* pw, const double* uv, int n,
+                      double cws[4][3], const double* ci, const double* cw, Cam cam, double* R, double* t) {
   double ccs[4][3] = {{0}};
   for (int i = 0; i < 4; ++i) {
     const double* v = ut + 12 * (11 - i);
     for (int j = 0; j < 4; ++j)
       for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[3 * j + k];
   }
+  /* solve_for_sign: the first point must lie in front of the camera */
+  double a0[4];
+  alphas_of(pw, cws, ci, a0);
+  const double z0 = a0[0] * ccs[0][2] + a0[1] * ccs[1][2] + a0[2] * ccs[2][2] + a0[3] * ccs[3][2];
+  const double sg = z0 < 0.0 ? -1.0 : 1.0;
+  double cc[3], H[9], err;
   for (int p = 0; p < n; ++p) {
     double a[4];
     alphas_of(pw + 3 * p, cws, ci, a);
     for (int k = 0; k < 3; ++k)
-      pcs_buf[3 * p + k] = a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k];
+      contrib_buf[3 * p + k] = sg * (a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k]);
   }
-  if (pcs_buf[2] < 0.0)
-    for (int p = 0; p < 3 * n; ++p) pcs_buf[p] = -pcs_buf[p];
-  procrustes(pw, pcs_buf, n, R, t);
-  double err = 0.0;
+  reduce_points(mode, n, 3, contrib_buf, cc);
+  for (int k = 0; k < 3; ++k) cc[k] /= n;
+  /* H = sum (pc - cc)(pw - cw)^T   (ABt in EPnP) */
+  for (int p = 0; p < n; ++p) {
+    double a[4], pc[3];
+    alphas_of(pw + 3 * p, cws, ci, a);
+    for (int k = 0; k < 3; ++k) pc[k] = sg * (a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k]);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) contrib_buf[9 * p + 3 * r + c] = (pc[r] - cc[r]) * (pw[3 * p + c] - cw[c]);
+  }
+  reduce_points(mode, n, 9, contrib_buf, H);
+  kabsch(H, R);
+  for (int r = 0; r < 3; ++r) t[r] = cc[r] - (R[r * 3 + 0] * cw[0] + R[r * 3 + 1] * cw[1] + R[r * 3 + 2] * cw[2]);
   for (int p = 0; p < n; ++p) {
     const double* X = pw + 3 * p;
     const double Xc = dot3(R, X) + t[0], Yc = dot3(R + 3, X) + t[1], Zc = dot3(R + 6, X) + t[2];
     const double iz = 1.0 / Zc;
     const double ue = cam.uc + cam.fu * Xc * iz, ve = cam.vc + cam.fv * Yc * iz;
     const double du = uv[2 * p] - ue, dv = uv[2 * p + 1] - ve;
-    err += sqrt(du * du + dv * dv);
+    contrib_buf[p] = sqrt(du * du + dv * dv);
   }
+  reduce_points(mode, n, 1, contrib_buf, &err);
   return err / n;
 }
 
-static double pcs_scratch[3 * MAXP];
-
-/* EPnP on n >= 4 correspondences (pw: n x 3 world, uv: n x 2 pixels). */
-static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R, double* t) {
-  double cws[4][3], ci[9];
-  ctrl_points(pw, n, cws, ci);
+/* EPnP on n >= 4 correspondences (pw: n x 3 world, uv: n x 2 pixels), sums in the kernel's `mode`. */
+static double epnp_mode(int mode, const double* pw, const double* uv, int n, Cam cam, double* R, double* t) {
+  double cws[4][3], ci[9], cw[3];
+  ctrl_points(mode, pw, n, cws, ci, cw);
   double MtM[144] = {0};
+  double G[4][144];
+  if (mode == SUM_WAVE) memset(G, 0, sizeof G);
   for (int p = 0; p < n; ++p) {
     double a[4];
     alphas_of(pw + 3 * p, cws, ci, a);
@@ -385,9 +455,12 @@ static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R
       r2[3 * j + 1] = a[j] * cam.fv;
       r2[3 * j + 2] = a[j] * (cam.vc - uv[2 * p + 1]);
     }
+    double* M = mode == SUM_WAVE ? G[p % 4] : MtM;
     for (int i = 0; i < 12; ++i)
-      for (int j = 0; j < 12; ++j) MtM[i * 12 + j] += r1[i] * r1[j] + r2[i] * r2[j];
+      for (int j = 0; j < 12; ++j) M[i * 12 + j] += r1[i] * r1[j] + r2[i] * r2[j];
   }
+  if (mode == SUM_WAVE)
+    for (int e = 0; e < 144; ++e) MtM[e] = (G[0][e] + G[1][e]) + (G[2][e] + G[3][e]);
   double v4[4][12], ut[144];
   jacobi12_par(MtM, v4);
   for (int q = 0; q < 4; ++q)
@@ -444,7 +517,7 @@ static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R
       betas[3] = betas[0] > 0 ? x[3] / betas[0] : 0.0;
     }
     gauss_newton(L, rho, betas);
-    errs[1] = r_and_t(ut, betas, pw, uv, n, cws, ci, cam, Rs[1], ts[1], pcs_scratch);
+    errs[1] = r_and_t(mode, ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[1], ts[1]);
   }
   /* approx 2: B11 B12 B22 from columns 0 1 2 */
   {
@@ -463,7 +536,7 @@ static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R
     betas[2] = 0.0;
     betas[3] = 0.0;
     gauss_newton(L, rho, betas);
-    errs[2] = r_and_t(ut, betas, pw, uv, n, cws, ci, cam, Rs[2], ts[2], pcs_scratch);
+    errs[2] = r_and_t(mode, ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[2], ts[2]);
   }
   /* approx 3: B11 B12 B22 B13 B23 from columns 0..4 */
   {
@@ -482,7 +555,7 @@ static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R
     betas[2] = betas[0] != 0.0 ? x[3] / betas[0] : 0.0;
     betas[3] = 0.0;
     gauss_newton(L, rho, betas);
-    errs[3] = r_and_t(ut, betas, pw, uv, n, cws, ci, cam, Rs[3], ts[3], pcs_scratch);
+    errs[3] = r_and_t(mode, ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[3], ts[3]);
   }
   int N = 1;
   if (errs[2] < errs[1]) N = 2;
@@ -490,6 +563,10 @@ static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R
   memcpy(R, Rs[N], sizeof(double) * 9);
   memcpy(t, ts[N], sizeof(double) * 3);
   return errs[N];
+}
+
+static double epnp(const double* pw, const double* uv, int n, Cam cam, double* R, double* t) {
+  return epnp_mode(SUM_SEQ, pw, uv, n, cam, R, t);
 }
 
 /* ---------------- public oracle entry points ---------------- */
@@ -538,7 +615,7 @@ void oracle_pnp_hypotheses(const float* obj, const float* img, int P, const floa
  * hypothesis, and returns the inlier count of the best hypothesis (0 = RANSAC failed).
  */
 int oracle_pnp_ransac(const float* obj, const float* img, int P, const float* K4, const int* subsets, int H,
-                      float thr, float conf, float* R_out, float* t_out, unsigned char* inlier_mask, int* best_h) {
+                      float thr, double conf, float* R_out, float* t_out, unsigned char* inlier_mask, int* best_h) {
   static double pw[3 * MAXP], uv[2 * MAXP];
   Cam cam = {K4[0], K4[1], K4[2], K4[3]};
   if (P > MAXP) P = MAXP;
@@ -571,7 +648,7 @@ int oracle_pnp_ransac(const float* obj, const float* img, int P, const float* K4
       best = h;
       memcpy(bestR, R, sizeof bestR);
       memcpy(bestt, t, sizeof bestt);
-      niters = ransac_update_niters((double)conf, (double)(P - cnt) / P, 5, niters);
+      niters = ransac_update_niters(conf, (double)(P - cnt) / P, 5, niters);
     }
   }
   if (best_h) *best_h = best;
@@ -598,7 +675,7 @@ int oracle_pnp_ransac(const float* obj, const float* img, int P, const float* K4
       ++n;
     }
   }
-  if (best >= 0 && n >= 5) epnp(pw, uv, n, cam, R, t);
+  if (best >= 0 && n >= 5) epnp_mode(SUM_WAVE, pw, uv, n, cam, R, t);
   for (int i = 0; i < 9; ++i) R_out[i] = (float)R[i];
   for (int i = 0; i < 3; ++i) t_out[i] = (float)t[i];
   return best >= 0 ? best_cnt : 0;

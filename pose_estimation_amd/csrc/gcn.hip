@@ -218,6 +218,10 @@ namespace {
 
 constexpr int kGcnThreads = 256;
 constexpr int kGcnKmax = 16;
+constexpr int kGcnSmax = 8;  // support_num bound of the LDS-staged 3-D form (the model uses 7)
+#ifndef GCN3_WAVES
+#define GCN3_WAVES 4  // waves per SIMD the 3-D form is register-bounded for (126 VGPRs, no spills)
+#endif
 
 // Block = 256 / LP points of one crop; a point is LP lanes, lane l owning channels 4l.. (+4 LP
 // per step when C > 4 LP). LP = 32 for C = 128 (levels 0 / 1: 8 points per block), LP = 128 for
@@ -294,8 +298,9 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
 #pragma unroll 1
     for (int s = 0; s < S; ++s) {
       const int so = s * C + c;
-      const float* dps = dp;
-      if constexpr (HAS_Y && !kHoist) asm volatile("" : "+v"(dps));
+      int dpo = p * kGcnKmax * D;
+      if constexpr (HAS_Y && !kHoist) asm volatile("" : "+v"(dpo));
+      const float* dps = sdir + dpo;
       f32x4 yv[HAS_Y ? KU : 1];
       if constexpr (HAS_Y) {
 #pragma unroll
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
       f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
       for (int j = 0; j < KU; ++j) {
-        if (!KC && j >= kk) break;
+        if (!KC && j >= kk) continue;  // predicated (a break here put yv in scratch memory)
         const float* dr = kHoist ? dreg + j * D : dps + j * D;
         f32x4 th = dr[0] * w[0];
 #pragma unroll
@@ -340,6 +345,112 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
   }
 }
 
+// Level-0 / level-1 form (3-D directions, C = 128, compile-time k): the same arithmetic as
+// gcn_conv_kernel<3, HAS_Y, KC, 32> (bit-identical outputs), laid out for occupancy and
+// memory-level parallelism instead of register reuse:
+//   * the normalised support directions dn [3][S*C] are staged in LDS once per block (10.5 KB),
+//     not re-read through L1 per support by every lane;
+//   * the neighbour rows are read with buffer loads: one 32-bit byte offset per neighbour (the
+//     crop's Y is one buffer resource) and the support as the scalar offset, so the support loop
+//     carries no 64-bit address arithmetic (the old form kept ten 64-bit pointers and stepped
+//     them every support: 228 VGPRs, 2 waves per SIMD);
+//   * __launch_bounds__(256, 4): >= 4 waves per SIMD, each with its k gather loads in flight.
+template <bool HAS_Y, int KC>
+__global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
+    const int* __restrict__ idx, int n, const float* __restrict__ v, long long v_bs, int v_st,
+    const float* __restrict__ dn, int S, const float* __restrict__ Y, const float* __restrict__ bn_s,
+    const float* __restrict__ bn_b, int relu, float* __restrict__ out, long long o_bs, int o_st) {
+  constexpr int C = 128, LP = 32, kPts = kGcnThreads / LP;
+  __shared__ f32x4 sdn[3 * kGcnSmax * C / 4];
+  __shared__ float sdir[kPts * KC * 3];
+  __shared__ int snb[kPts * KC];
+  const int gx = gridDim.x;
+  const int lin = krrn_xcd_remap(blockIdx.x + gx * blockIdx.y, gx * gridDim.y);
+  const int b = lin / gx;
+  const int p0 = (lin - b * gx) * kPts;
+  const int np = min(kPts, n - p0);
+  const float* vb = v + b * v_bs;
+  const int SC = S * C;
+  for (int e = threadIdx.x; e < 3 * SC / 4; e += kGcnThreads) sdn[e] = reinterpret_cast<const f32x4*>(dn)[e];
+  for (int e = threadIdx.x; e < np * KC; e += kGcnThreads) {
+    const int p = e / KC, j = e - (e / KC) * KC;
+    const int pi = p0 + p;
+    const int nj = idx[((long long)b * n + pi) * KC + j];
+    snb[p * KC + j] = nj;
+    float dv[3];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      dv[i] = vb[(long long)nj * v_st + i] - vb[(long long)pi * v_st + i];
+      ss += dv[i] * dv[i];
+    }
+    const float nr = fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) sdir[(p * KC + j) * 3 + i] = dv[i] / nr;
+  }
+  __syncthreads();
+  const int p = threadIdx.x / LP, l = threadIdx.x % LP;
+  if (p >= np) return;
+  const int pi = p0 + p;
+  const int c = 4 * l;
+  const int yrow = (S + 1) * C;
+  const int dpo = p * KC * 3;  // this point's directions in sdir
+  __amdgpu_buffer_rsrc_t rs;
+  if constexpr (HAS_Y)
+    rs = __builtin_amdgcn_make_buffer_rsrc((void*)(Y + (long long)b * n * yrow), (short)0, n * yrow * 4, 0x00020000);
+  const int npo = p * KC;  // this point's neighbour rows in snb
+  const unsigned cbyte = (unsigned)((C + c) * 4);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int s = 0; s < S; ++s) {
+    f32x4 yv[HAS_Y ? KC : 1];
+    if constexpr (HAS_Y) {
+      // neighbour rows re-read from LDS (broadcast) every support: 10 fewer live VGPRs. The
+      // offset (not a pointer) is made opaque, so the reads stay ds_read on the LDS array
+      int nbo = npo;
+      asm volatile("" : "+v"(nbo));
+#pragma unroll
+      for (int j = 0; j < KC; ++j)
+        yv[j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(snb[nbo + j] * yrow * 4) + cbyte, s * C * 4, 0));
+    }
+    f32x4 w[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = sdn[(i * SC + s * C + c) >> 2];
+    // the directions are re-read from LDS (broadcast) every support: hoisted they cost 30 VGPRs
+    int dro = dpo;
+    asm volatile("" : "+v"(dro));
+    const float* dreg = sdir + dro;
+    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      f32x4 th = dreg[j * 3] * w[0];
+#pragma unroll
+      for (int i = 1; i < 3; ++i) th += dreg[j * 3 + i] * w[i];
+      if constexpr (HAS_Y) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) th[q] = fmaxf(th[q], 0.f);
+        th *= yv[j];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], th[q]);
+    }
+    if constexpr (!HAS_Y) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], 0.f);
+    }
+    acc += m;
+  }
+  f32x4 o = acc;
+  if constexpr (HAS_Y) o = *reinterpret_cast<const f32x4*>(Y + (long long)b * n * yrow + (long long)pi * yrow + c) + o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (bn_s) o[q] = o[q] * bn_s[c + q] + bn_b[c + q];
+    if (relu) o[q] = fmaxf(o[q], 0.f);
+  }
+  *reinterpret_cast<f32x4*>(out + b * o_bs + (long long)pi * o_st + c) = o;
+}
+
 }  // namespace
 
 KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, long long v_bs, int v_st, int d,
@@ -356,6 +467,23 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   const bool wide = C >= 512;  // LP = 128 lanes per point (see the kernel comment)
   dim3 grid(krrn_cdiv(n, wide ? kGcnThreads / 128 : kGcnThreads / 32), B);
   hipStream_t s = (hipStream_t)stream;
+  static const int legacy = [] {
+    const char* e = getenv("KRRN_GCN_LEGACY");  // 1: the register-hoisted form for every level
+    return e ? atoi(e) : 0;
+  }();
+  if (!legacy && d == 3 && C == 128 && S <= kGcnSmax && (k == 10 || k == 8) &&
+      (long long)n * (S + 1) * C * 4 < (1LL << 31)) {
+#define KRRN_GCN3(HY, KC) \
+  hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
+                     bn_scale, bn_bias, relu, out, o_bs, o_st)
+    if (Y) {
+      if (k == 10) KRRN_GCN3(true, 10); else KRRN_GCN3(true, 8);
+    } else {
+      if (k == 10) KRRN_GCN3(false, 10); else KRRN_GCN3(false, 8);
+    }
+#undef KRRN_GCN3
+    return krrn_launch_status();
+  }
 #define KRRN_GCN_LAUNCH(DD, HY, KC)                                                                        \
   if (wide)                                                                                                \
     hipLaunchKernelGGL((gcn_conv_kernel<DD, HY, KC, 128>), grid, dim3(kGcnThreads), 0, s, idx, n, k, v,   \

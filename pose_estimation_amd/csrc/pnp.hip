@@ -115,12 +115,19 @@ __device__ __forceinline__ double shfl_f64(double v, int src) {
   return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-// v[i] for a per-lane i: select chain (a runtime index into a register array would go to scratch)
+// v[i] for a per-lane i: select chain. Each element passes through an empty asm first: otherwise
+// LLVM folds the chain back into a dynamically indexed load, which puts the array in scratch memory
+// (the round-2 kernels' 1 KB / lane of scratch came from exactly this).
 template <int N>
 __device__ __forceinline__ double pick(const double (&v)[N], int i) {
   double r = v[0];
+  asm volatile("" : "+v"(r));
 #pragma unroll
-  for (int j = 1; j < N; ++j) r = (i == j) ? v[j] : r;
+  for (int j = 1; j < N; ++j) {
+    double x = v[j];
+    asm volatile("" : "+v"(x));
+    r = (i == j) ? x : r;
+  }
   return r;
 }
 
@@ -152,21 +159,17 @@ __device__ __forceinline__ double group_sum16(double v) {
   return v;
 }
 
-__device__ __forceinline__ void eig12_group(const double (&m)[78], double (&v4)[48]) {
+// In: lane r's row of M^T M (zero in lanes 12..15). Out: vq[q] = component r of the eigenvector of
+// the q-th smallest eigenvalue (ascending, ties: lower column first) -- each lane keeps its own
+// components only (the old form broadcast all 48 into every lane: 96 VGPRs).
+__device__ __forceinline__ void eig12_rows(const double (&row)[12], double (&vq)[4]) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63, r = lane & 15, base = lane & ~15;
   const bool act = r < 12;
   double a[12], u[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    double v = 0.0;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const int lo = i < j ? i : j, hi = i < j ? j : i;
-      const int e = lo * 12 - lo * (lo - 1) / 2 + (hi - lo);  // packed upper triangle, row-major
-      v = (r == i) ? m[e] : v;
-    }
-    a[j] = v;
+    a[j] = row[j];
     u[j] = (r == j) ? 1.0 : 0.0;
   }
   for (int sweep = 0; sweep < 40; ++sweep) {
@@ -185,7 +188,7 @@ __device__ __forceinline__ void eig12_group(const double (&m)[78], double (&v4)[
 #pragma unroll
     for (int k = 0; k < 11; ++k) {
       const int pr = act ? rr_partner(k, r) : r;
-      const int lo = r < pr ? r : pr, hi = r < pr ? pr : r;
+      const int lo = r < pr ? r : pr;
       const double d = pick(a, r);                            // own diagonal
       const double apq = shfl_f64(pick(a, pr), base + lo);    // a[lo][hi], from lane lo
       const double dp = shfl_f64(d, base + pr);               // partner's diagonal
@@ -234,8 +237,8 @@ __device__ __forceinline__ void eig12_group(const double (&m)[78], double (&v4)[
   const double wd = pick(a, r);
 #pragma unroll
   for (int i = 0; i < 12; ++i) w[i] = shfl_f64(wd, base + i);
-  // the 4 smallest eigenvalues in ascending order (ties: lower column first)
   unsigned used = 0;
+#pragma unroll
   for (int q4 = 0; q4 < 4; ++q4) {
     int mi = -1;
     double wm = 0.0;
@@ -245,31 +248,37 @@ __device__ __forceinline__ void eig12_group(const double (&m)[78], double (&v4)[
       if (mi < 0 || w[j] < wm) { mi = j; wm = w[j]; }
     }
     used |= 1u << mi;
-    const double um = pick(u, mi);
-#pragma unroll
-    for (int kk = 0; kk < 12; ++kk) v4[q4 * 12 + kk] = shfl_f64(um, base + kk);
+    vq[q4] = pick(u, mi);
   }
 }
 
-// least squares min ||A x - b|| (A is 6 x N) through the pseudo-inverse from eig(A^T A)
+// Least squares min ||A x - b|| for the 6 x N system whose row k lives in lane k of the group
+// (arow, brow; lanes >= 6 hold duplicates that are never read): the normal equations gathered row
+// by row in order k = 0..5 (the expression order of oracle/pnp_ref.c), then replicated in every
+// lane: Cholesky when A has full column rank (the usual case), else the pseudo-inverse from
+// eig(A^T A) (OpenCV solves these with CV_SVD).
 template <int N>
-__device__ __forceinline__ void lsq_solve(const double (&A)[6 * N], const double (&b)[6], double (&x)[N]) {
-  double AtA[N * N], w[N], V[N * N], Atb[N];
+__device__ __forceinline__ void lsq_rows(const double (&arow)[N], double brow, double (&x)[N]) {
+#pragma clang fp contract(off)
+  const int base = (threadIdx.x & 63) & ~15;
+  double AtA[N * N], Atb[N];
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
+  for (int i = 0; i < N * N; ++i) AtA[i] = 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      double s = 0.0;
+  for (int i = 0; i < N; ++i) Atb[i] = 0.0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) s += A[k * N + i] * A[k * N + j];
-      AtA[i * N + j] = s;
+  for (int k = 0; k < 6; ++k) {
+    double ak[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) ak[i] = shfl_f64(arow[i], base + k);
+    const double bk = shfl_f64(brow, base + k);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) AtA[i * N + j] += ak[i] * ak[j];
+      Atb[i] += ak[i] * bk;
     }
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) s += A[k * N + i] * b[k];
-    Atb[i] = s;
   }
-  // Full column rank (the usual case): Cholesky of the normal equations, ~N^3/6 flops.
   double C[N * N];
   double dmax = 0.0;
 #pragma unroll
@@ -309,7 +318,7 @@ __device__ __forceinline__ void lsq_solve(const double (&A)[6 * N], const double
     }
     return;
   }
-  // rank deficient: pseudo-inverse (OpenCV solves these with CV_SVD)
+  double w[N], V[N * N];
   eig_small<N>(AtA, w, V);
   const double tol = (w[0] > 0 ? w[0] : 0.0) * 1e-24;
 #pragma unroll
@@ -350,59 +359,8 @@ __device__ __forceinline__ void pinv3(const double (&a)[9], double (&r)[9]) {
     for (int j = 0; j < 3; ++j) r[i * 3 + j] = Pm[i * 3] * a[j * 3] + Pm[i * 3 + 1] * a[j * 3 + 1] + Pm[i * 3 + 2] * a[j * 3 + 2];
 }
 
+
 __device__ __forceinline__ double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-
-// Correspondences in LDS; `list` (optional) selects a subset.
-struct Pts {
-  const float* obj;  // [P][3]
-  const float* img;  // [P][2]
-  const int* list;   // nullptr -> identity
-  int n;
-  __device__ __forceinline__ int id(int i) const { return list ? list[i] : i; }
-  __device__ __forceinline__ void pw(int i, double* p) const {
-    const float* o = obj + 3 * id(i);
-    p[0] = o[0]; p[1] = o[1]; p[2] = o[2];
-  }
-  __device__ __forceinline__ void uv(int i, double* q) const {
-    const float* o = img + 2 * id(i);
-    q[0] = o[0]; q[1] = o[1];
-  }
-};
-
-// Point-loop sums and the 12x12 solve of EPnP, evaluated either per 16-lane group (a RANSAC
-// hypothesis: GroupSum, the point sums replicated in every lane) or by one wave with the points
-// spread over the 64 lanes and a butterfly reduction (the refinement on all inliers, WaveSum).
-// The small dense algebra between the sums is replicated in every lane; the 12x12 solve is
-// eig12_group in each 16-lane group (WaveSum: all 4 groups solve the same replicated matrix).
-struct WaveSum {
-  int lane;
-  template <int NV, class F>
-  __device__ __forceinline__ void operator()(int n, F f, double (&acc)[NV]) const {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-    for (int i = lane; i < n; i += 64) f(i, acc);
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      double v = acc[k];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-      acc[k] = v;
-    }
-  }
-  __device__ __forceinline__ void eig12(const double (&m)[78], double (&v4)[48]) const { eig12_group(m, v4); }
-};
-
-// One RANSAC hypothesis per aligned 16-lane group: the point sums (5 points) replicated in every
-// lane, the 12x12 solve spread over the group (eig12_group).
-struct GroupSum {
-  template <int NV, class F>
-  __device__ __forceinline__ void operator()(int n, F f, double (&acc)[NV]) const {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-    for (int i = 0; i < n; ++i) f(i, acc);
-  }
-  __device__ __forceinline__ void eig12(const double (&m)[78], double (&v4)[48]) const { eig12_group(m, v4); }
-};
 
 __device__ __forceinline__ void alphas_of(const double* p, const double cws[4][3], const double* ci, double a[4]) {
   const double d0 = p[0] - cws[0][0], d1 = p[1] - cws[0][1], d2 = p[2] - cws[0][2];
@@ -412,24 +370,136 @@ __device__ __forceinline__ void alphas_of(const double* p, const double cws[4][3
   a[0] = 1.0 - a[1] - a[2] - a[3];
 }
 
-__device__ __forceinline__ void gauss_newton(const double (&L)[60], const double (&rho)[6], double (&betas)[4]) {
+// Lane r's entries of row r of M^T M for one point: the two rows of M per point are
+// r1 = [a_j fu, 0, a_j (uc - u)], r2 = [0, a_j fv, a_j (vc - v)] (j = 0..3).
+__device__ __forceinline__ void mtm_row_add(const double* X, const double* q, const double cws[4][3], const double* ci,
+                                            const Cam& cam, int r, double (&acc)[12]) {
+  double a[4];
+  alphas_of(X, cws, ci, a);
+  double r1[12], r2[12];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r1[3 * j] = a[j] * cam.fu;
+    r1[3 * j + 1] = 0.0;
+    r1[3 * j + 2] = a[j] * (cam.uc - q[0]);
+    r2[3 * j] = 0.0;
+    r2[3 * j + 1] = a[j] * cam.fv;
+    r2[3 * j + 2] = a[j] * (cam.vc - q[1]);
+  }
+  const double r1r = pick(r1, r), r2r = pick(r2, r);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) acc[j] += r1r * r1[j] + r2r * r2[j];
+}
+
+// Point sums of EPnP. HypSum: one RANSAC hypothesis per aligned 16-lane group, its 5 points in
+// order in every lane (the point indices are registers, so the loop is unrolled at compile time).
+// WaveSum: the refinement on all inliers by one wave, points strided over the 64 lanes then a fixed
+// butterfly (identical in every lane); M^T M rows strided over the 4 groups, then (g0 + g1) +
+// (g2 + g3). oracle/pnp_ref.c restates both orders.
+struct HypSum {
+  const float* obj;  // LDS [P][3]
+  const float* img;  // LDS [P][2]
+  int ids[5];
+  static constexpr int n = 5;
+  __device__ __forceinline__ void pt(int i, double* X, double* q) const {
+    const float* o = obj + 3 * ids[i];
+    X[0] = o[0]; X[1] = o[1]; X[2] = o[2];
+    const float* u = img + 2 * ids[i];
+    q[0] = u[0]; q[1] = u[1];
+  }
+  template <int NV, class F>
+  __device__ __forceinline__ void operator()(F f, double (&acc)[NV]) const {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      double X[3], q[2];
+      pt(i, X, q);
+      f(X, q, acc);
+    }
+  }
+  __device__ __forceinline__ int count() const { return 5; }
+  __device__ __forceinline__ void rows(const double cws[4][3], const double* ci, const Cam& cam, double (&acc)[12]) const {
+    const int r = threadIdx.x & 15;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) acc[j] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      double X[3], q[2];
+      pt(i, X, q);
+      mtm_row_add(X, q, cws, ci, cam, r, acc);
+    }
+    if (r >= 12) {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) acc[j] = 0.0;
+    }
+  }
+};
+
+struct WaveSum {
+  const float* obj;
+  const float* img;
+  const int* list;  // LDS: the inlier indices
+  int n;
+  __device__ __forceinline__ void pt(int i, double* X, double* q) const {
+    const int id = list[i];
+    const float* o = obj + 3 * id;
+    X[0] = o[0]; X[1] = o[1]; X[2] = o[2];
+    const float* u = img + 2 * id;
+    q[0] = u[0]; q[1] = u[1];
+  }
+  template <int NV, class F>
+  __device__ __forceinline__ void operator()(F f, double (&acc)[NV]) const {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    for (int i = lane; i < n; i += 64) {
+      double X[3], q[2];
+      pt(i, X, q);
+      f(X, q, acc);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double v = acc[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      acc[k] = v;
+    }
+  }
+  __device__ __forceinline__ int count() const { return n; }
+  __device__ __forceinline__ void rows(const double cws[4][3], const double* ci, const Cam& cam, double (&acc)[12]) const {
+    const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) acc[j] = 0.0;
+    for (int i = g; i < n; i += 4) {
+      double X[3], q[2];
+      pt(i, X, q);
+      mtm_row_add(X, q, cws, ci, cam, r, acc);
+    }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      double v = acc[j];
+      v = v + __shfl_xor(v, 16);
+      v = v + __shfl_xor(v, 32);
+      acc[j] = r < 12 ? v : 0.0;
+    }
+  }
+};
+
+__device__ __forceinline__ void gauss_newton(const double (&Lr)[10], double rho_r, double (&betas)[4]) {
 #pragma unroll 1
   for (int it = 0; it < 5; ++it) {
-    double A[24], b[6], x[4];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const double* l = L + 10 * i;
-      double* a = A + 4 * i;
-      a[0] = 2 * l[0] * betas[0] + l[1] * betas[1] + l[3] * betas[2] + l[6] * betas[3];
-      a[1] = l[1] * betas[0] + 2 * l[2] * betas[1] + l[4] * betas[2] + l[7] * betas[3];
-      a[2] = l[3] * betas[0] + l[4] * betas[1] + 2 * l[5] * betas[2] + l[8] * betas[3];
-      a[3] = l[6] * betas[0] + l[7] * betas[1] + l[8] * betas[2] + 2 * l[9] * betas[3];
-      b[i] = rho[i] - (l[0] * betas[0] * betas[0] + l[1] * betas[0] * betas[1] + l[2] * betas[1] * betas[1] +
-                       l[3] * betas[0] * betas[2] + l[4] * betas[1] * betas[2] + l[5] * betas[2] * betas[2] +
-                       l[6] * betas[0] * betas[3] + l[7] * betas[1] * betas[3] + l[8] * betas[2] * betas[3] +
-                       l[9] * betas[3] * betas[3]);
-    }
-    lsq_solve<4>(A, b, x);
+    const double* l = Lr;
+    double a[4], x[4];
+    a[0] = 2 * l[0] * betas[0] + l[1] * betas[1] + l[3] * betas[2] + l[6] * betas[3];
+    a[1] = l[1] * betas[0] + 2 * l[2] * betas[1] + l[4] * betas[2] + l[7] * betas[3];
+    a[2] = l[3] * betas[0] + l[4] * betas[1] + 2 * l[5] * betas[2] + l[8] * betas[3];
+    a[3] = l[6] * betas[0] + l[7] * betas[1] + l[8] * betas[2] + 2 * l[9] * betas[3];
+    const double b = rho_r - (l[0] * betas[0] * betas[0] + l[1] * betas[0] * betas[1] + l[2] * betas[1] * betas[1] +
+                              l[3] * betas[0] * betas[2] + l[4] * betas[1] * betas[2] + l[5] * betas[2] * betas[2] +
+                              l[6] * betas[0] * betas[3] + l[7] * betas[1] * betas[3] + l[8] * betas[2] * betas[3] +
+                              l[9] * betas[3] * betas[3]);
+    lsq_rows<4>(a, b, x);
 #pragma unroll
     for (int k = 0; k < 4; ++k) betas[k] += x[k];
   }
@@ -473,58 +543,52 @@ __device__ __forceinline__ void kabsch(const double (&H)[9], double (&R)[9]) {
     for (int c = 0; c < 3; ++c) R[r * 3 + c] = U[r] * V[c] + U[3 + r] * V[3 + c] + U[6 + r] * v2[c];
 }
 
+// R, t from betas (lane r holds component r of the 4 null-space vectors: vq); returns the mean
+// reprojection error.
 template <class SUM>
-__device__ double r_and_t(const SUM& sum, const double (&v4)[48], const double (&betas)[4], const Pts& P,
-                          const double cws[4][3], const double* ci, const double* cw, const Cam& cam, double (&R)[9],
-                          double (&t)[3]) {
+__device__ double r_and_t(const SUM& sum, const double (&vq)[4], const double (&betas)[4], const double cws[4][3],
+                          const double* ci, const double* cw, const Cam& cam, double (&R)[9], double (&t)[3]) {
+  const int base = (threadIdx.x & 63) & ~15;
+  double cr = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) cr += betas[i] * vq[i];
   double ccs[4][3];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) ccs[j][k] = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v4[12 * i + 3 * j + k];
+    for (int k = 0; k < 3; ++k) ccs[j][k] = shfl_f64(cr, base + 3 * j + k);
   // solve_for_sign: the first point must lie in front of the camera
-  double p0[3], a0[4];
-  P.pw(0, p0);
+  double p0[3], q0[2], a0[4];
+  sum.pt(0, p0, q0);
   alphas_of(p0, cws, ci, a0);
   const double z0 = a0[0] * ccs[0][2] + a0[1] * ccs[1][2] + a0[2] * ccs[2][2] + a0[3] * ccs[3][2];
   const double sg = z0 < 0.0 ? -1.0 : 1.0;
-  const int n = P.n;
+  const int n = sum.count();
   double cc[3];
-  sum(n, [&](int i, double (&acc)[3]) {
-        double p[3], a[4];
-        P.pw(i, p);
-        alphas_of(p, cws, ci, a);
+  sum([&](const double* X, const double*, double (&acc)[3]) {
+        double a[4];
+        alphas_of(X, cws, ci, a);
 #pragma unroll
         for (int k = 0; k < 3; ++k) acc[k] += sg * (a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k]);
       }, cc);
 #pragma unroll
   for (int k = 0; k < 3; ++k) cc[k] /= n;
   double H[9];
-  sum(n, [&](int i, double (&acc)[9]) {
-        double p[3], a[4], pc[3];
-        P.pw(i, p);
-        alphas_of(p, cws, ci, a);
+  sum([&](const double* X, const double*, double (&acc)[9]) {
+        double a[4], pc[3];
+        alphas_of(X, cws, ci, a);
 #pragma unroll
         for (int k = 0; k < 3; ++k) pc[k] = sg * (a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k]);
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
-          for (int c = 0; c < 3; ++c) acc[r * 3 + c] += (pc[r] - cc[r]) * (p[c] - cw[c]);
+          for (int c = 0; c < 3; ++c) acc[r * 3 + c] += (pc[r] - cc[r]) * (X[c] - cw[c]);
       }, H);
   kabsch(H, R);
 #pragma unroll
   for (int r = 0; r < 3; ++r) t[r] = cc[r] - (R[r * 3 + 0] * cw[0] + R[r * 3 + 1] * cw[1] + R[r * 3 + 2] * cw[2]);
   double err[1];
-  sum(n, [&](int i, double (&acc)[1]) {
-        double X[3], q[2];
-        P.pw(i, X);
-        P.uv(i, q);
+  sum([&](const double* X, const double* q, double (&acc)[1]) {
         const double Xc = dot3(R, X) + t[0], Yc = dot3(R + 3, X) + t[1], Zc = dot3(R + 6, X) + t[2];
         const double iz = 1.0 / Zc;
         const double du = q[0] - (cam.uc + cam.fu * Xc * iz), dv = q[1] - (cam.vc + cam.fv * Yc * iz);
@@ -533,24 +597,25 @@ __device__ double r_and_t(const SUM& sum, const double (&v4)[48], const double (
   return err[0] / n;
 }
 
-// EPnP (Lepetit et al. 2009) on the points of P; result R (row-major), t.
+// EPnP (Lepetit et al. 2009) over the points of `sum`, spread over an aligned 16-lane group: the
+// point sums and the small dense algebra replicated in every lane, the rows of M^T M, of the 6 x 10
+// L matrix and of every 6 x N least-squares system one per lane, the 12 x 12 eigen-solve shared
+// (eig12_rows). Result R (row-major), t, identical in every lane of the group.
 template <class SUM>
-__device__ void epnp(const SUM& sum, const Pts& P, const Cam& cam, double (&Rout)[9], double (&tout)[3]) {
-  const int n = P.n;
+__device__ void epnp(const SUM& sum, const Cam& cam, double (&Rout)[9], double (&tout)[3]) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63, r = lane & 15, base = lane & ~15;
+  const int n = sum.count();
   double cws[4][3], ci[9], cw[3];
   {
-    sum(n, [&](int i, double (&acc)[3]) {
-          double p[3];
-          P.pw(i, p);
-          acc[0] += p[0]; acc[1] += p[1]; acc[2] += p[2];
+    sum([&](const double* X, const double*, double (&acc)[3]) {
+          acc[0] += X[0]; acc[1] += X[1]; acc[2] += X[2];
         }, cw);
 #pragma unroll
     for (int j = 0; j < 3; ++j) cw[j] /= n;
     double C6[6];
-    sum(n, [&](int i, double (&acc)[6]) {
-          double p[3];
-          P.pw(i, p);
-          const double d0 = p[0] - cw[0], d1 = p[1] - cw[1], d2 = p[2] - cw[2];
+    sum([&](const double* X, const double*, double (&acc)[6]) {
+          const double d0 = X[0] - cw[0], d1 = X[1] - cw[1], d2 = X[2] - cw[2];
           acc[0] += d0 * d0; acc[1] += d0 * d1; acc[2] += d0 * d2;
           acc[3] += d1 * d1; acc[4] += d1 * d2; acc[5] += d2 * d2;
         }, C6);
@@ -574,79 +639,51 @@ __device__ void epnp(const SUM& sum, const Pts& P, const Cam& cam, double (&Rout
 #pragma unroll
     for (int i = 0; i < 9; ++i) ci[i] = CI[i];
   }
-  // M^T M from the two rows per point: r1 = [a_j fu, 0, a_j (uc - u)], r2 = [0, a_j fv, a_j (vc - v)]
-  double m[78];
-  sum(n, [&](int p, double (&acc)[78]) {
-        double X[3], q[2], a[4];
-        P.pw(p, X);
-        P.uv(p, q);
-        alphas_of(X, cws, ci, a);
-        double r1[12], r2[12];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          r1[3 * j] = a[j] * cam.fu;
-          r1[3 * j + 1] = 0.0;
-          r1[3 * j + 2] = a[j] * (cam.uc - q[0]);
-          r2[3 * j] = 0.0;
-          r2[3 * j + 1] = a[j] * cam.fv;
-          r2[3 * j + 2] = a[j] * (cam.vc - q[1]);
-        }
-        int e = 0;
-#pragma unroll
-        for (int i = 0; i < 12; ++i)
-#pragma unroll
-          for (int j = i; j < 12; ++j, ++e) acc[e] += r1[i] * r1[j] + r2[i] * r2[j];
-      }, m);
-  double v4[48];
-  sum.eig12(m, v4);
-  double L[60], rho[6];
+  double vq[4];
   {
-    double dv[4][6][3];
+    double mrow[12];
+    sum.rows(cws, ci, cam, mrow);
+    eig12_rows(mrow, vq);
+  }
+  // lane i < 6: row i of L (6 x 10) and rho[i]; pair (a, b) of control points per row
+  const int li = r < 6 ? r : 5;
+  const int pa = li < 3 ? 0 : (li < 5 ? 1 : 2);
+  const int pb = li < 3 ? li + 1 : (li < 5 ? li - 1 : 3);
+  double Lr[10], rho_r;
+  {
+    double dv[4][3];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double* v = v4 + 12 * i;
-      int a = 0, b = 1;
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dv[i][j][k] = v[3 * a + k] - v[3 * b + k];
-        if (++b > 3) { ++a; b = a + 1; }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      double* r = L + 10 * i;
-      r[0] = dot3(dv[0][i], dv[0][i]);
-      r[1] = 2.0 * dot3(dv[0][i], dv[1][i]);
-      r[2] = dot3(dv[1][i], dv[1][i]);
-      r[3] = 2.0 * dot3(dv[0][i], dv[2][i]);
-      r[4] = 2.0 * dot3(dv[1][i], dv[2][i]);
-      r[5] = dot3(dv[2][i], dv[2][i]);
-      r[6] = 2.0 * dot3(dv[0][i], dv[3][i]);
-      r[7] = 2.0 * dot3(dv[1][i], dv[3][i]);
-      r[8] = 2.0 * dot3(dv[2][i], dv[3][i]);
-      r[9] = dot3(dv[3][i], dv[3][i]);
-    }
+      for (int k = 0; k < 3; ++k) dv[q][k] = shfl_f64(vq[q], base + 3 * pa + k) - shfl_f64(vq[q], base + 3 * pb + k);
+    Lr[0] = dot3(dv[0], dv[0]);
+    Lr[1] = 2.0 * dot3(dv[0], dv[1]);
+    Lr[2] = dot3(dv[1], dv[1]);
+    Lr[3] = 2.0 * dot3(dv[0], dv[2]);
+    Lr[4] = 2.0 * dot3(dv[1], dv[2]);
+    Lr[5] = dot3(dv[2], dv[2]);
+    Lr[6] = 2.0 * dot3(dv[0], dv[3]);
+    Lr[7] = 2.0 * dot3(dv[1], dv[3]);
+    Lr[8] = 2.0 * dot3(dv[2], dv[3]);
+    Lr[9] = dot3(dv[3], dv[3]);
+    double rho6[6];
     int a = 0, b = 1;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const double d0 = cws[a][0] - cws[b][0], d1 = cws[a][1] - cws[b][1], d2 = cws[a][2] - cws[b][2];
-      rho[j] = d0 * d0 + d1 * d1 + d2 * d2;
+      rho6[j] = d0 * d0 + d1 * d1 + d2 * d2;
       if (++b > 3) { ++a; b = a + 1; }
     }
+    rho_r = pick(rho6, li);
   }
   double best_err = 1e300;
 #pragma unroll 1
   for (int approx = 1; approx <= 3; ++approx) {
     double betas[4] = {0, 0, 0, 0};
     if (approx == 1) {
-      double A[24], x[4];
-      const int cols[4] = {0, 1, 3, 6};
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) A[4 * i + j] = L[10 * i + cols[j]];
-      lsq_solve<4>(A, rho, x);
+      const double arow[4] = {Lr[0], Lr[1], Lr[3], Lr[6]};
+      double x[4];
+      lsq_rows<4>(arow, rho_r, x);
       if (x[0] < 0) {
         betas[0] = sqrt(-x[0]);
 #pragma unroll
@@ -657,12 +694,9 @@ __device__ void epnp(const SUM& sum, const Pts& P, const Cam& cam, double (&Rout
         for (int k = 1; k < 4; ++k) betas[k] = betas[0] > 0 ? x[k] / betas[0] : 0.0;
       }
     } else if (approx == 2) {
-      double A[18], x[3];
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) A[3 * i + j] = L[10 * i + j];
-      lsq_solve<3>(A, rho, x);
+      const double arow[3] = {Lr[0], Lr[1], Lr[2]};
+      double x[3];
+      lsq_rows<3>(arow, rho_r, x);
       if (x[0] < 0) {
         betas[0] = sqrt(-x[0]);
         betas[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
@@ -672,12 +706,9 @@ __device__ void epnp(const SUM& sum, const Pts& P, const Cam& cam, double (&Rout
       }
       if (x[1] < 0) betas[0] = -betas[0];
     } else {
-      double A[30], x[5];
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) A[5 * i + j] = L[10 * i + j];
-      lsq_solve<5>(A, rho, x);
+      const double arow[5] = {Lr[0], Lr[1], Lr[2], Lr[3], Lr[4]};
+      double x[5];
+      lsq_rows<5>(arow, rho_r, x);
       if (x[0] < 0) {
         betas[0] = sqrt(-x[0]);
         betas[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
@@ -688,9 +719,9 @@ __device__ void epnp(const SUM& sum, const Pts& P, const Cam& cam, double (&Rout
       if (x[1] < 0) betas[0] = -betas[0];
       betas[2] = betas[0] != 0.0 ? x[3] / betas[0] : 0.0;
     }
-    gauss_newton(L, rho, betas);
+    gauss_newton(Lr, rho_r, betas);
     double R[9], t[3];
-    const double err = r_and_t(sum, v4, betas, P, cws, ci, cw, cam, R, t);
+    const double err = r_and_t(sum, vq, betas, cws, ci, cw, cam, R, t);
     if (approx == 1 || err < best_err) {
       best_err = err;
 #pragma unroll
@@ -733,12 +764,10 @@ __device__ void load_corr(int b, const float* xyz, int HW, const long long* choo
   }
 }
 
-// Phase 1: one RANSAC hypothesis per 16-lane group, 16 per block, grid (B, ceil(H / 16)). The
-// group replicates the hypothesis' 5-point EPnP over its lanes except the 12x12 solve, which it
-// shares (eig12_group), and splits the P inlier tests over its 16 lanes. Writes the f32 pose (R,
-// t: the precision the inlier test uses) and the inlier count of every hypothesis. LDS: the P
-// correspondences only (5 KB at P = 256), so the blocks co-reside with the fusion / TBase
-// launches they run beside.
+// Phase 1: one RANSAC hypothesis per 16-lane group, 16 per block, grid (B, ceil(H / 16)). Writes the
+// f32 pose (R, t: the precision the inlier test uses) and the inlier count of every hypothesis. LDS:
+// the P correspondences only (5 KB at P = 256), so the blocks co-reside with the fusion / TBase
+// launches they run beside; no scratch memory (every register array has compile-time indices).
 constexpr int kHypPerBlock = 16;
 __global__ __launch_bounds__(256) void pnp_hyp_kernel(
     const float* __restrict__ xyz, int HW, const long long* __restrict__ choose, int N, const int* __restrict__ sel,
@@ -755,13 +784,17 @@ __global__ __launch_bounds__(256) void pnp_hyp_kernel(
   const int r = threadIdx.x & 15;
   const int h = blockIdx.y * kHypPerBlock + (threadIdx.x >> 4);
   const int hs = h < H ? h : H - 1;  // a tail group solves a duplicate (whole groups stay active) and writes nothing
-  int ids[5];
-  for (int i = 0; i < 5; ++i) ids[i] = subsets[((long long)b * H + hs) * 5 + i];
-  Pts sub{sobj, simg, ids, 5};
+  HypSum sub;
+  sub.obj = sobj;
+  sub.img = simg;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sub.ids[i] = subsets[((long long)b * H + hs) * 5 + i];
   double R[9], t[3];
-  epnp(GroupSum{}, sub, cam, R, t);
+  epnp(sub, cam, R, t);
   float Rf[9], tf[3];
+#pragma unroll
   for (int i = 0; i < 9; ++i) Rf[i] = (float)R[i];
+#pragma unroll
   for (int i = 0; i < 3; ++i) tf[i] = (float)t[i];
   const float thr2 = thr * thr;
   int cnt = 0;
@@ -770,7 +803,9 @@ __global__ __launch_bounds__(256) void pnp_hyp_kernel(
   for (int off = 8; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
   if (h >= H || r != 0) return;
   float* o = hyp_pose + ((long long)b * H + h) * 12;
+#pragma unroll
   for (int i = 0; i < 9; ++i) o[i] = Rf[i];
+#pragma unroll
   for (int i = 0; i < 3; ++i) o[9 + i] = tf[i];
   hyp_cnt[(long long)b * H + h] = cnt;
 }
@@ -791,11 +826,12 @@ __device__ __forceinline__ int ransac_update_niters(double conf, double ep, int 
 // order: hypothesis h is considered while h < niters; a strictly better count (and >= 5 inliers:
 // goodCount > max(maxGoodCount, modelPoints - 1)) becomes the best and lowers niters to
 // RANSACUpdateNumIters(confidence, outlier ratio, 5, niters). Then the best hypothesis' ordered
-// inlier set and EPnP on all inliers with the point sums spread over the 64 lanes.
+// inlier set and EPnP on all inliers (WaveSum: the point sums spread over the 64 lanes, each of the 4
+// lane groups solving the same replicated system).
 __global__ __launch_bounds__(64) void pnp_refine_kernel(
     const float* __restrict__ xyz, int HW, const long long* __restrict__ choose, int N, const int* __restrict__ sel,
     int P, const float* __restrict__ xmap, const float* __restrict__ ymap, const float* __restrict__ K4,
-    const double* __restrict__ extent, const double* __restrict__ lfb, int H, float thr, float conf,
+    const double* __restrict__ extent, const double* __restrict__ lfb, int H, float thr, double conf,
     const float* __restrict__ hyp_pose, const int* __restrict__ hyp_cnt, float* __restrict__ Rout,
     float* __restrict__ tout, int* __restrict__ inl_out, unsigned char* __restrict__ mask_out) {
   __shared__ float sobj[kPnpMaxP * 3];
@@ -815,16 +851,18 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
       if (cnt > (best_cnt > 4 ? best_cnt : 4)) {
         best_cnt = cnt;
         best_h = h0 + i;
-        niters = ransac_update_niters((double)conf, (double)(P - cnt) / P, 5, niters);
+        niters = ransac_update_niters(conf, (double)(P - cnt) / P, 5, niters);
       }
     }
   }
   const bool ok = best_h >= 0;
   float Rf[9], tf[3];
-  if (ok) {
-    const float* hp = hyp_pose + ((long long)b * H + best_h) * 12;
-    for (int i = 0; i < 9; ++i) Rf[i] = hp[i];
-    for (int i = 0; i < 3; ++i) tf[i] = hp[9 + i];
+  {
+    const float* hp = hyp_pose + ((long long)b * H + (ok ? best_h : 0)) * 12;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rf[i] = ok ? hp[i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) tf[i] = ok ? hp[9 + i] : 0.f;
   }
   const float thr2 = thr * thr;
   // ordered compaction of the inliers: ballot per 64-point chunk + prefix popcount
@@ -840,11 +878,13 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
   }
   __syncthreads();
   if (ok && n >= 5) {
-    Pts inl{sobj, simg, slist, n};
+    const WaveSum inl{sobj, simg, slist, n};
     double R[9], t[3];
-    epnp(WaveSum{lane}, inl, cam, R, t);
+    epnp(inl, cam, R, t);
     if (lane == 0) {
+#pragma unroll
       for (int i = 0; i < 9; ++i) Rout[9 * b + i] = (float)R[i];
+#pragma unroll
       for (int i = 0; i < 3; ++i) tout[3 * b + i] = (float)t[i];
     }
   } else if (lane == 0) {
@@ -860,13 +900,13 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
 
 KRRN_API int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choose, int N, const int* sel, int P,
                                  const float* xmap, const float* ymap, const float* K4, const double* extent,
-                                 const double* lfborder, const int* subsets, int H, float thr, float conf,
+                                 const double* lfborder, const int* subsets, int H, float thr, double conf,
                                  float* workspace, float* R, float* t, int* inliers, unsigned char* inlier_mask, int B,
                                  void* stream) {
   if (!xyz || !choose || !sel || !xmap || !ymap || !K4 || !extent || !lfborder || !subsets || !workspace || !R ||
       !t || !inliers)
     return KRRN_EARG;
-  if (B < 1 || P < 5 || P > kPnpMaxP || H < 1 || H > 4095 || N < 1 || HW < 1 || !(conf >= 0.f && conf <= 1.f))
+  if (B < 1 || P < 5 || P > kPnpMaxP || H < 1 || H > 4095 || N < 1 || HW < 1 || !(conf >= 0.0 && conf <= 1.0))
     return KRRN_ESHAPE;
   hipStream_t s = (hipStream_t)stream;
   float* hyp_pose = workspace;

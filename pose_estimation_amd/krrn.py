@@ -46,6 +46,9 @@ from .runtime import Late, Plan, add_conv, ptr
 
 
 TBASE_EARLY = os.environ.get("KRRN_TBASE_EARLY", "1") == "1"
+# KRRN.forward replays a hipGraph of its plan (captured after one serial warm-up run): the only
+# form in which the plan's side streams run concurrently (runtime.Plan); 0 = serial eager runs
+GRAPH = os.environ.get("KRRN_GRAPH", "1") == "1"
 
 
 class KRRNPlan:
@@ -194,6 +197,8 @@ class KRRNPlan:
         if pose_hook is not None:
             plan.join([psid])
         self.env = {"cls": self.cls, "cloud": self.cloud}
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.warm = False
         self.nbytes = plan_bytes(plan) + plan_bytes(getattr(self, "device_perm_plan", None))
 
     def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):
@@ -237,7 +242,25 @@ class KRRNPlan:
             raise ValueError(f"perm_mode {mode!r}")
 
     def run(self):
-        self.plan.run(self.env)
+        """One forward on the caller's stream: the first call runs the plan serially (warm-up),
+        the second captures it (side streams as graph branches), every later call replays."""
+        if not GRAPH:
+            self.plan.run(self.env)
+            return
+        if self.graph is not None:
+            self.graph.replay()
+            return
+        if not self.warm:
+            self.plan.run(self.env)
+            self.warm = True
+            return
+        cur = torch.cuda.current_stream(self.plan.device)
+        cur.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.plan.run(self.env, serial=False)
+        self.graph = g
+        g.replay()
 
     def outputs(self, model: "KRRN") -> Dict[str, Optional[torch.Tensor]]:
         C = model.num_cls

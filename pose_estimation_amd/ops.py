@@ -286,6 +286,19 @@ def gemm_weights_x3(wt: torch.Tensor) -> torch.Tensor:
     return c.permute(0, 2, 4, 3, 1, 5).contiguous()                 # nb g q fh nl 4
 
 
+def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:
+    """GEMM weights [N][K] f32 (scale folded) -> the wave fragments krrn_gemm_panel_x3_f32 reads: int32
+    [N/32][K/8][3][64][4]. Fragment (column tile nb, 8-k group g, quad q) is one coalesced 1-KB wave
+    load: lane fh*32 + nl holds, for column 32 nb + nl and k = 8 g + 4 fh .. + 3, the quad q of the
+    split terms: q = 0 [h0..h3 m0..m3] (x the activations' [h m]: hh + mm), q = 1 [m0..m3 h0..h3]
+    (x [h m]: hm + mh), q = 2 [l0..l3 h0..h3] (x [h l]: hl + lh). N % 32 == 0, K % 8 == 0."""
+    N, K = wt.shape
+    h, m, l = (t.reshape(N, K // 4, 4) for t in split_bf16x3(wt))
+    c = torch.cat([h, m, m, h, l, h], dim=-1).contiguous()  # [N][K/4][24] bf16 = q0 | q1 | q2
+    c = c.view(torch.int32).reshape(N // 32, 32, K // 8, 2, 3, 4)  # nb nl g fh q 4
+    return c.permute(0, 2, 4, 3, 1, 5).contiguous()                 # nb g q fh nl 4
+
+
 def wino_eligible(spec: ConvSpec, M: int) -> bool:
     """Fused Winograd for the wide stride-1 3x3 convs (>= 32 channels in and out, >= 32k output
     pixels); the narrow HRNet branches stay on the implicit GEMM (latency-bound there)."""

@@ -116,9 +116,11 @@ class BatchPipeline:
         pt.kp.plan.run(pt.kp.env, serial=serial)
         pt.pose.run({}, serial=serial)
 
-    def run(self, serial: bool = False):
-        """Enqueue one step on the current stream (micro-batches fork onto their streams and
-        join back)."""
+    def run(self, concurrent: bool = False):
+        """Enqueue one step on the current stream. Eagerly everything runs serially on it; with
+        `concurrent` (used under hipGraph capture only, see runtime.Plan) the plans' side streams
+        and the micro-batches' streams fork and join back."""
+        serial = not concurrent
         if not self.streams or serial:
             for pt in self.parts:
                 self._run_part(pt, serial)
@@ -142,7 +144,7 @@ class BatchPipeline:
         torch.cuda.synchronize(self.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.run()
+            self.run(concurrent=True)
         torch.cuda.synchronize(self.device)
 
     def step(self):
@@ -215,13 +217,13 @@ class PipelinedPipeline:
         for s in self.slots:
             s.load(data)
 
-    def _run_a(self, slot: int):
+    def _run_a(self, slot: int, concurrent: bool = False):
         for p, env in self.stage_a[slot]:
-            p.run(dict(env))
+            p.run(dict(env), serial=not concurrent)
 
-    def _run_b(self, slot: int):
+    def _run_b(self, slot: int, concurrent: bool = False):
         for p, env in self.stage_b[slot]:
-            p.run(dict(env))
+            p.run(dict(env), serial=not concurrent)
 
     def _prime(self):
         """Stage A of both slots once, so the first half-step's stage B has backbone features."""
@@ -246,9 +248,22 @@ class PipelinedPipeline:
         self.h = 0
 
     def run(self):
+        """One eager half-step: stage B of slot h, THEN stage A of the other slot, both on the
+        caller's stream (no concurrency between the two slots' launch lists).
+
+        Run side by side eagerly, the two slots' plans enqueue onto ~14 HIP streams, more than the
+        GPU_MAX_HW_QUEUES = 4 hardware queues the runtime multiplexes them onto; under that sharing
+        a stage-B kernel intermittently consumed an input its own stream's previous kernel had not
+        finished publishing (profiles/race_bisect.py, DESIGN.md §5: 4/5 mismatching half-steps with
+        4 hardware queues, 0/5 with 16, 0/5 with either stage on one stream, 0/5 sequential, 0/5 as
+        captured hipGraphs). The concurrent form is the graph replay (`step` after `capture`);
+        eagerly each stage also runs serially (runtime.Plan.run)."""
         if not self.primed:
             self._prime()
-        self._half(self._run_a, self._run_b)
+        b, a = self.h, self.h ^ 1
+        self._run_b(b)
+        self._run_a(a)
+        self.h ^= 1
 
     def capture(self):
         """Warm up every stage once on a side stream, then capture one hipGraph per stage and slot."""
@@ -266,7 +281,7 @@ class PipelinedPipeline:
             for gs, fn in ((self.graphs_b, self._run_b), (self.graphs_a, self._run_a)):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    fn(i)
+                    fn(i, concurrent=True)
                 gs[i] = g
         torch.cuda.synchronize(self.device)
         # the captures above do not execute: slot state is as after the warm-up (A of both slots

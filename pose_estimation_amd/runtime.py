@@ -22,6 +22,7 @@ from . import _lib, ops
 P = ctypes.c_void_p
 I = ctypes.c_int
 F = ctypes.c_float
+D = ctypes.c_double
 L = ctypes.c_longlong
 U = ctypes.c_uint
 
@@ -37,7 +38,7 @@ _lib.register("krrn_points_gather_f32", [P, P, P, P, I, I, I, I, P, P])
 _lib.register("krrn_gather_rows_f32", [P, I, L, I, P, L, I, P, L, I, I, I, P])
 _lib.register("krrn_tbase_tail_f32", [P, I, I, I, P, P, P, P, P, P])
 _lib.register("krrn_gather2_add_f32", [P, P, L, I, P, P, L, I, I, I, P, P, P, I, P, L, I, I, P])
-_lib.register("krrn_pnp_ransac_f32", [P, I, P, I, P, I, P, P, P, P, P, P, I, F, F, P, P, P, P, P, I, P])
+_lib.register("krrn_pnp_ransac_f32", [P, I, P, I, P, I, P, P, P, P, P, P, I, F, D, P, P, P, P, P, I, P])
 _lib.register("krrn_randperm_i32", [P, U, I, I, I, P, P])
 _lib.register("krrn_ransac_subsets", [P, U, I, I, I, P, P])
 _lib.register("krrn_randperm_multi_i32", [P, I, P, P, P, P, P])
@@ -56,6 +57,7 @@ _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])
 _lib.register("krrn_gemm_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, L, L, L, P])
+_lib.register("krrn_gemm_panel_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, P])
 
 
 class ConvDesc(ctypes.Structure):
@@ -132,7 +134,13 @@ class Plan:
     Ops are tagged with a stream id (`on_stream`); id 0 is the caller's current stream and ids
     1.. are plan-owned side streams, ordered by explicit `fork` / `join` points. Independent
     HRNet branches and head towers use this to run concurrently (one small conv cannot fill 256
-    CUs; four of them side by side fill more). `run(serial=True)` puts everything on stream 0."""
+    CUs; four of them side by side fill more).
+
+    `run()` is serial by default (everything on the caller's stream). The side streams are used
+    only with `run(serial=False)` under hipGraph capture, where every fork / join becomes a graph
+    edge: run eagerly, the plan's ~7 streams share the GPU_MAX_HW_QUEUES = 4 hardware queues, and
+    under that sharing a kernel intermittently read an input its producer on another stream had
+    not finished (profiles/race_bisect.py) -- the captured graphs never did."""
 
     def __init__(self, device: torch.device):
         self.device = device
@@ -197,7 +205,7 @@ class Plan:
         env["__streams__"] = None if serial else streams
         return main
 
-    def run(self, env: Dict[str, Any], serial: bool = False):
+    def run(self, env: Dict[str, Any], serial: bool = True):
         self._streams(env, serial)
         for op in self.ops:
             op(env)
@@ -400,6 +408,9 @@ BLAS_MAX_WS = 64 << 20
 # level-0 GCN GEMMs: 198 vs 180 us, output-write-bound) and slower at layer1's K = 64 (all
 # eligible GEMMs on gemm_x3: 1.98 vs 1.77 ms of GEMMs per step)
 GEMM_X3 = os.environ.get("KRRN_GEMM_X3", "1") == "1"
+# short-K GEMMs (K = 64 / 128, N % 32 == 0, one row group) on the A-stationary split-bf16 kernel
+# (gemm_panel.hip): the level-0 / level-1 GCN GEMMs, whose 262 MB output makes them write streams
+GEMM_PANEL = os.environ.get("KRRN_GEMM_PANEL", "1") == "1"
 GEMM_X3_MINK = int(os.environ.get("KRRN_GEMM_X3_MINK", "256"))
 
 
@@ -423,15 +434,27 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
              r_grp: int = 0, cin: Optional[int] = None, cout: Optional[int] = None, tag: str = "gemm") -> bool:
     """Append a plain GEMM out[m, n] = act(scale[n] * (A[m] . wt[n]) + bias[n] (+ res[m, n])) on hipBLASLt
     (krrn_blas_gemm_*; scale folded into the weights). Returns False when hipBLASLt is disabled
-    (KRRN_BLAS=0) or rejects the problem: the caller then emits its own kernel."""
-    if not BLAS:
-        return False
+    (KRRN_BLAS=0) or rejects the problem: the caller then emits its own kernel. Short-K GEMMs go to
+    the A-stationary split-bf16 kernel and K >= 256 ones to gemm_x3 first (own kernels)."""
     dev = plan.device
     w = wt.reshape(N, -1)[:, :K].float()
     if scale is not None:
         w = w * scale.reshape(N, 1).to(w.device)
     w = w.contiguous()
     flops = 2.0 * (cin or K) * (cout or N) * M * batch
+    if GEMM_PANEL and K in (64, 128) and N % 32 == 0 and batch == 1 and lda % 4 == 0 and a_off % 4 == 0:
+        wp = ops.gemm_weights_panel(w)
+        plan.buffers.append([wp, bias])
+        rows = (M + 127) // 128
+        csplit = 1
+        while rows * csplit < 512 and (N // 32) % (2 * csplit) == 0:  # fill the chip: >= 512 blocks
+            csplit *= 2
+        plan.add("krrn_gemm_panel_x3_f32", P(a.data_ptr() + 4 * a_off), lda, M, K, N, ptr(wp), ptr(bias), ptr(res),
+                 ldr, ptr(out), ldo, int(relu), csplit,
+                 meta=dict(kernel="gemm_panel_x3", flops=flops, tag=tag, M=M, N=N, K=K, splits=csplit,
+                           mfma_flops=2.0 * M * N * K * 6 / 16, mfma_bf16_flops=2.0 * M * N * K * 6,
+                           bytes=4.0 * (M * K + M * N)))
+        return True
     if GEMM_X3 and K >= GEMM_X3_MINK and K % 32 == 0 and N % 128 == 0 and lda % 4 == 0 and ldo % 4 == 0 and a_off % 4 == 0 \
             and (res is None or ldr % 4 == 0):
         # own split-bf16 GEMM (gemm_x3.hip): 6 bf16 term products per f32 product
@@ -442,6 +465,8 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
                  meta=dict(kernel="gemm_x3", flops=flops, tag=tag, M=M * batch, N=N, K=K, splits=1,
                            mfma_flops=2.0 * M * batch * N * K * 6 / 16, mfma_bf16_flops=2.0 * M * batch * N * K * 6))
         return True
+    if not BLAS:
+        return False
     h = ctypes.c_void_p()
     wsb = ctypes.c_longlong()
     st = _lib.lib().krrn_blas_gemm_create(M, N, K, lda, ldo, batch, a_grp, o_grp, int(bias is not None), int(relu),

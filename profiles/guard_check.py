@@ -47,6 +47,10 @@ pl = BatchPipeline(m, B, S, N, dev, parts=1, seed=0)
 pl.load(d)
 pl.run()
 torch.cuda.synchronize()
+pl.capture()  # and the multi-stream graph replayed (the bench's form)
+for _ in range(3):
+    pl.step()
+torch.cuda.synchronize()
 bad = 0
 for raw, nb, shape, dtype, where in records:
     g = raw[nb:]

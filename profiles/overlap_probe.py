@@ -2,7 +2,7 @@
 the other slot) when the two hipGraphs are replayed on two streams? Times A alone, B alone, A then
 B on one stream, and A || B on two streams (the PipelinedPipeline half-step).
 
-usage (GPU box): python3 profiles/overlap_test.py
+usage (GPU box): python3 profiles/overlap_probe.py
 """
 import os
 import sys

@@ -68,6 +68,8 @@ def krrn_case(num_cls, objlist, B, S, N, bseed, wseed, pseed):
         "region_s4": out["region"][:, :, ::4, ::4].contiguous().numpy(),
         "pred_t": out["pred_t"].numpy(),
         "feat_s8": tr["feat"][:, ::8, :1280].contiguous().numpy(),
+        # the pooled level-2 vertices the 9-D idx2 kNN runs on (tie justification of idx2 flips)
+        "pool_2": tr["pool_2"].contiguous().numpy(),
     }
     for i, p in enumerate(perms):
         rec[f"perm{i}"] = p.numpy().astype(np.int32)

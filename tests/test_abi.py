@@ -56,6 +56,6 @@ def test_host_side_errors():
                                fake, 4, 0, 8, 8, 1, 1, 0, 0, 0, 0, 0, 1, N, N) == -3
     # pnp: P < 5 -> KRRN_ESHAPE
     assert lib.krrn_pnp_ransac_f32(fake, 16, fake, 10, fake, 4, fake, fake, fake, fake, fake, fake, 10,
-                                   ctypes.c_float(1.0), ctypes.c_float(0.9999), fake, fake, fake, fake, N, 1, N) == -2
+                                   ctypes.c_float(1.0), ctypes.c_double(0.9999), fake, fake, fake, fake, N, 1, N) == -2
     with pytest.raises(RuntimeError, match="KRRN_EARG"):
         _lib.check(-1, "x")

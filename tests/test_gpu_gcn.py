@@ -66,3 +66,34 @@ def test_gcn_conv_layer(dev, B, n, k, mode):
                                    ptr(d_b), 1, ptr(out), n * C, C, B, st), "gcn conv")
     torch.cuda.synchronize()
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("B,n,k,has_y", [(4, 1000, 10, False), (2, 250, 8, True), (2, 77, 8, False),
+                                         (3, 64, 10, True)])
+def test_gcn_conv_surface_and_k8(dev, B, n, k, has_y):
+    """Conv_surface (gcn3d.py:88-112: no Y, ReLU(max_k theta) summed over supports, no BN) and the
+    k = 8 level-1 form of the test shapes, through the LDS-staged 3-D kernel."""
+    S, C = 7, 128
+    g = torch.Generator().manual_seed(n * 17 + k + int(has_y))
+    idx = _idx(B, n, k, "local", g)
+    v = torch.randn(B, n, 9, generator=g)
+    dn = torch.randn(3, S * C, generator=g)
+    dn = dn / dn.norm(dim=0, keepdim=True)
+    bi = torch.arange(B)[:, None, None]
+    if has_y:
+        Y = torch.randn(B, n, (S + 1) * C, generator=g)
+        ref = _torch_conv_layer(idx, v[..., :3], dn, Y, S, C, torch.ones(C), torch.zeros(C), False)
+    else:
+        Y = None
+        d = v[bi, idx.long(), :3] - v[:, :, None, :3]
+        d = d / d.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        ref = torch.relu((d @ dn).max(dim=2).values).view(B, n, S, C).sum(dim=2)
+    L = _lib.lib()
+    st = P(torch.cuda.current_stream().cuda_stream)
+    d_idx, d_v, d_dn = idx.to(dev), v.to(dev), dn.contiguous().to(dev)
+    d_Y = Y.to(dev) if has_y else None
+    out = torch.full((B, n, C), float("nan"), device=dev)
+    _lib.check(L.krrn_gcn_conv_f32(ptr(d_idx), n, k, ptr(d_v), n * 9, 9, 3, ptr(d_dn), S, C, ptr(d_Y), P(0), P(0), 0,
+                                   ptr(out), n * C, C, B, st), "gcn conv")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=2e-5)

@@ -13,11 +13,13 @@ from pose_estimation_amd.config import make_config
 from pose_estimation_amd.krrn import KRRN
 from pose_estimation_amd.runtime import P, ptr
 from pose_estimation_amd.synthetic import init_weights
+from tests.parity import knn_flips_at_ties
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 MAP_RTOL = 2e-4
-T_ATOL = 1e-5
+T_ATOL = 1e-6       # pred_t when every discrete decision agrees with the fixture (north_star: 1e-3 mm)
+T_ATOL_FLIP = 5e-5  # ... when a 9-D idx2 kNN entry flipped at a distance tie (justified below)
 
 
 def _load(name):
@@ -43,14 +45,20 @@ def test_krrn_golden(dev, name):
     for k in ("xyz", "normal", "mask"):
         assert _rel(out[k].cpu().numpy(), g[k]) < MAP_RTOL, k
     assert _rel(out["region"][:, :, ::4, ::4].cpu().numpy(), g["region_s4"]) < MAP_RTOL
-    assert np.abs(out["pred_t"].cpu().numpy() - g["pred_t"]).max() < T_ATOL
     B, _, N = g["choose"].shape
     plan = m.get_plan(B, g["img"].shape[2], N, True)
     fb = plan.fusion_bufs
     for k in ("idx0", "idx1", "nn1", "nn2"):
         got = fb[k].cpu().numpy().reshape(g[k].shape)
         assert np.array_equal(got, g[k]), k
-    assert (fb["idx2"].cpu().numpy().reshape(g["idx2"].shape) == g["idx2"]).mean() > 0.9
+    # idx2 is decided on predicted (pooled 9-D) coordinates: an entry may differ only at a distance
+    # tie within the coordinate perturbation + the kNN's own f32 rounding (tests/parity.py)
+    n_bad, n_tie = knn_flips_at_ties(fb["idx2"].cpu().reshape(g["idx2"].shape), torch.from_numpy(g["idx2"]),
+                                     fb["PV2"].cpu(), torch.from_numpy(g["pool_2"]), None, "idx2")
+    assert n_bad == n_tie, (n_bad, n_tie)
+    t_err = float(np.abs(out["pred_t"].cpu().numpy() - g["pred_t"]).max())
+    print(f"pred_t |err| {t_err:.2e} m, idx2 flips at ties: {n_tie}")
+    assert t_err < (T_ATOL if n_bad == 0 else T_ATOL_FLIP), t_err
     assert _rel(plan.feat[:, ::8].cpu().numpy(), g["feat_s8"]) < 5e-3
 
 
@@ -86,8 +94,8 @@ def test_pnp_golden(dev):
                                    sel=p("sel"), subsets=p("subsets"), return_info=True)
         torch.cuda.synchronize()
         cnt = int(info["inliers"][0])
-        # noisy scene: f64 rounding (GPU vs gcc) may flip points sitting on the 1 px threshold
-        tol_cnt, tol = (8, 1e-2) if i == 1 else (0, 1e-5)
-        assert abs(cnt - int(g[f"s{i}_inliers"][0])) <= tol_cnt, (i, cnt)
-        assert np.abs(R.cpu().numpy() - g[f"s{i}_R"]).max() < tol, i
-        assert np.abs(t.cpu().numpy() - g[f"s{i}_t"]).max() < tol, i
+        # the oracle restates the kernel's f64 expression order (oracle/pnp_ref.c): the same inlier
+        # count and the pose to f32 rounding on every scene, the noisy one included
+        assert cnt == int(g[f"s{i}_inliers"][0]), (i, cnt)
+        assert np.abs(R.cpu().numpy() - g[f"s{i}_R"]).max() < 1e-6, i
+        assert np.abs(t.cpu().numpy() - g[f"s{i}_t"]).max() < 1e-6, i

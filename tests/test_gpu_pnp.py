@@ -82,22 +82,13 @@ def test_known_pose_recovery(dev):
     assert (info["inliers"].cpu().numpy() >= 200).all()
 
 
-@pytest.mark.parametrize("noise_px,cnt_tol,pose_tol", [(0.0, 0, 1e-4), (0.4, 8, 1e-2)])
+@pytest.mark.parametrize("noise_px,cnt_tol,pose_tol", [(0.0, 0, 1e-4), (0.4, 0, 1e-4)])
 def test_matches_oracle_same_subsets(dev, noise_px, cnt_tol, pose_tol):
-    """RANSAC vs the C oracle on identical subsets.
-
-    A 5-point EPnP system M (10 x 12) has a >= 2-dimensional null space, and the eigenvectors of
-    a repeated (zero) eigenvalue are defined only up to a basis choice, which differs between any
-    two eigen-solvers (GPU Jacobi vs gcc Jacobi, or vs OpenCV's). For outlier-contaminated
-    subsets the resulting hypothesis poses are therefore arbitrary on both sides (measured
-    |dR| up to 1.9 on low-count hypotheses) and not comparable. What is comparable:
-      (1) the oracle run on the GPU's selected subset reproduces its inlier count and final
-          (refined) pose -- hypothesis scoring, inlier compaction and the all-inlier EPnP;
-          exactly on noiseless data; with 0.4 px noise the selected 5-point pose itself carries
-          the basis ambiguity at noise level, which moves points sitting on the 1 px threshold;
-      (2) the GPU's RANSAC is as good as the oracle's over all subsets: which near-best subset
-          wins is chaotic on both sides (noisy crops measured: either side ahead by up to ~6%
-          on single crops), so this is asserted on the batch total."""
+    """RANSAC vs the C oracle on identical subsets: the oracle run on the GPU's selected subset
+    reproduces its inlier count exactly and its refined pose within 1e-4 (north_star's R bound),
+    noiseless and with 0.4 px noise; and the GPU's RANSAC over all subsets is as good as the
+    oracle's over the batch. (The full hypothesis-by-hypothesis comparison is
+    test_full_ransac_matches_oracle.)"""
     B, N, S = 16, 1000, 100
     xyz, data, _, _ = _scene(B, N, S, 1, outlier_frac=0.3, noise_px=noise_px)
     R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
@@ -186,3 +177,37 @@ def test_device_rng_multi_matches_single(dev):
     bad = (ctypes.c_int * c)(*([5000] * c))
     assert _lib.lib().krrn_randperm_multi_i32(ptr(seed), c, sids, bad, ks, outs, st) < 0
     assert _lib.lib().krrn_randperm_multi_i32(ptr(seed), 9, sids, ns, ks, outs, st) < 0
+
+
+@pytest.mark.parametrize("noise_px,outliers", [(0.0, 0.3), (0.4, 0.3), (1.0, 0.5)])
+def test_full_ransac_matches_oracle(dev, noise_px, outliers):
+    """Every one of the H = 100 hypotheses, the RANSAC selection and the refined pose vs the C oracle
+    on identical subsets. oracle/pnp_ref.c restates the kernel's f64 expression order: the 5-point
+    EPnP of a hypothesis sums its points in order (HypSum), the all-inlier refinement in the wave's
+    order (WaveSum: 64 lane partials + butterfly; M^T M rows by lane group), the normal equations
+    solved by Cholesky, the 12 x 12 eigen-solve by the same parallel Jacobi schedule -- so the
+    hypothesis inlier counts are equal count for count, the selected hypothesis is the same, and
+    R / t agree to 1e-6 (north_star: 1e-4 on R). cv2.solvePnPRansac itself is not installable
+    here: parity to OpenCV is unpinned (oracle/pnp_ref.c header)."""
+    B, N, S = 16, 1000, 100
+    xyz, data, _, _ = _scene(B, N, S, 7, outlier_frac=outliers, noise_px=noise_px)
+    R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
+    torch.cuda.synchronize()
+    sel = info["sel"].cpu().long()
+    subs = info["subsets"].cpu()
+    H = subs.shape[1]
+    hcnt = info["workspace"].cpu()[B * H * 12:].view(torch.int32)[:B * H].view(B, H).numpy()
+    worst = 0.0
+    for b in range(B):
+        s = sel[b]
+        pix = data["choose"][b, 0, s]
+        obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
+        img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
+        _, _, ocnt = opnp.pnp_hypotheses(obj, img, K4, subs[b].numpy(), 1.0)
+        assert np.array_equal(ocnt, hcnt[b]), (b, np.nonzero(ocnt != hcnt[b])[0][:8])
+        Ro, to, cnt, mask, best = opnp.pnp_ransac(obj, img, K4, subs[b].numpy(), 1.0)
+        assert int(info["inliers"][b]) == cnt, (b, int(info["inliers"][b]), cnt)
+        assert np.array_equal(info["mask"][b].cpu().numpy().astype(bool), mask), b
+        worst = max(worst, float(np.abs(R[b].cpu().numpy() - Ro).max()), float(np.abs(t[b].cpu().numpy() - to).max()))
+    print(f"noise {noise_px} px, {outliers:.0%} outliers: max |dR|, |dt| vs oracle {worst:.2e}")
+    assert worst < 1e-6, worst
