@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
 //     carries no 64-bit address arithmetic (the old form kept ten 64-bit pointers and stepped
 //     them every support: 228 VGPRs, 2 waves per SIMD);
 //   * __launch_bounds__(256, 4): >= 4 waves per SIMD, each with its k gather loads in flight.
-template <bool HAS_Y, int KC>
+template <bool HAS_Y, int KC, bool BUF = true>
 __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     const int* __restrict__ idx, int n, const float* __restrict__ v, long long v_bs, int v_st,
     const float* __restrict__ dn, int S, const float* __restrict__ Y, const float* __restrict__ bn_s,
@@ -410,9 +410,14 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
       int nbo = npo;
       asm volatile("" : "+v"(nbo));
 #pragma unroll
-      for (int j = 0; j < KC; ++j)
-        yv[j] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(snb[nbo + j] * yrow * 4) + cbyte, s * C * 4, 0));
+      for (int j = 0; j < KC; ++j) {
+        if constexpr (BUF)
+          yv[j] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(snb[nbo + j] * yrow * 4) + cbyte, s * C * 4, 0));
+        else
+          yv[j] = *reinterpret_cast<const f32x4*>(Y + (long long)b * n * yrow + (long long)snb[nbo + j] * yrow + C + c +
+                                                  s * C);
+      }
     }
     f32x4 w[3];
 #pragma unroll
@@ -467,19 +472,30 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   const bool wide = C >= 512;  // LP = 128 lanes per point (see the kernel comment)
   dim3 grid(krrn_cdiv(n, wide ? kGcnThreads / 128 : kGcnThreads / 32), B);
   hipStream_t s = (hipStream_t)stream;
+  // KRRN_GCN_LEGACY: 1 = the register-hoisted form for every level; 2 = only for the convs with Y;
+  // 3 = only for the surface convs (diagnostics). KRRN_GCN3_BUF=0: plain global loads of Y rows.
   static const int legacy = [] {
-    const char* e = getenv("KRRN_GCN_LEGACY");  // 1: the register-hoisted form for every level
+    const char* e = getenv("KRRN_GCN_LEGACY");
     return e ? atoi(e) : 0;
   }();
-  if (!legacy && d == 3 && C == 128 && S <= kGcnSmax && (k == 10 || k == 8) &&
+  static const int bufload = [] {
+    const char* e = getenv("KRRN_GCN3_BUF");
+    return e ? atoi(e) : 1;
+  }();
+  const bool use3 = legacy == 0 || (legacy == 2 && !Y) || (legacy == 3 && Y);
+  if (use3 && d == 3 && C == 128 && S <= kGcnSmax && (k == 10 || k == 8) &&
       (long long)n * (S + 1) * C * 4 < (1LL << 31)) {
-#define KRRN_GCN3(HY, KC) \
-  hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
+#define KRRN_GCN3(HY, KC, BF) \
+  hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC, BF>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
                      bn_scale, bn_bias, relu, out, o_bs, o_st)
     if (Y) {
-      if (k == 10) KRRN_GCN3(true, 10); else KRRN_GCN3(true, 8);
+      if (bufload) {
+        if (k == 10) KRRN_GCN3(true, 10, true); else KRRN_GCN3(true, 8, true);
+      } else {
+        if (k == 10) KRRN_GCN3(true, 10, false); else KRRN_GCN3(true, 8, false);
+      }
     } else {
-      if (k == 10) KRRN_GCN3(false, 10); else KRRN_GCN3(false, 8);
+      if (k == 10) KRRN_GCN3(false, 10, true); else KRRN_GCN3(false, 8, true);
     }
 #undef KRRN_GCN3
     return krrn_launch_status();

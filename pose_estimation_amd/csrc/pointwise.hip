@@ -226,7 +226,7 @@ __global__ void gather_rows_kernel(const void* __restrict__ idx, long long idx_b
 // pred_t[b] = mean_i( cloud[b, i] + W4[0:3] . h[b, i] + b4[0:3] )   (one block per crop)
 // TBase conv4 (C -> 3, +bias) and pred_t = mean_N(cloud + t_res) (posenet.py:80, krrn.py:150-153).
 // One block of 16 waves per crop (the B = 64 blocks cannot fill the chip, so each brings 256 points
-// into flight per pass: 77 -> ~25 us per launch); 4 lanes per point, each lane a float4 stripe of the
+// into flight per pass: 77 -> 36 us per launch measured in the step); 4 lanes per point, each lane a float4 stripe of the
 // C-channel row (a wave reads 16 rows x 64 contiguous bytes per load), 2 shuffles finish the dot
 // product. The mean is a fixed-order reduction (per-lane partials, then a fixed tree), so runs are
 // bit-reproducible.

@@ -257,6 +257,10 @@ class _LinemodTree:
                                    "t": np.array(e["cam_t_m2c"], np.float64) / 1000.0,
                                    "bbox": [float(v) for v in e["obj_bb"]]})
             pts = ply_vtx(os.path.join(root, "models", f"obj_{obj:02d}.ply")) / 1000.0
+            if len(pts) < n_model_pts:
+                # the reference's random.sample(range(len(pts)), len(pts) - num_pt_mesh_large) raises here
+                # too (batchdataset.py:700-704): every crop's ADD(-S) runs over exactly n_model_pts points
+                raise ValueError(f"obj_{obj:02d}.ply has {len(pts)} vertices < num_pt_mesh_large = {n_model_pts}")
             if len(pts) > n_model_pts:  # random deletion down to num_pt_mesh_large (:700-704)
                 keep = np.sort(rng.choice(len(pts), n_model_pts, replace=False))
                 pts = pts[keep]
@@ -372,8 +376,10 @@ class PoseDataset(torch.utils.data.Dataset):
         lfb = [np.array(info[m[0]]["min"]) / 1000.0 for m in metas]
         R64 = torch.from_numpy(np.stack([m[1] for m in metas]))
         t64 = torch.from_numpy(np.stack([m[2] for m in metas]))
-        npt = min(len(m[3]) for m in metas)
-        mp = torch.from_numpy(np.stack([m[3][:npt] for m in metas]))
+        # every object keeps exactly num_pt_mesh_large model points (_LinemodTree / synthetic_frames), so
+        # a batch mixing objects stacks them without cutting any crop's ADD(-S) point set
+        assert len({len(m[3]) for m in metas}) == 1, [len(m[3]) for m in metas]
+        mp = torch.from_numpy(np.stack([m[3] for m in metas]))
         host = {
             "cls_id": torch.tensor([[self.objlist.index(m[0])] for m in metas], dtype=torch.int64),
             "intrinsic": K4,

@@ -159,7 +159,10 @@ def test_epoch(model: KRRN, dataset: PoseDataset, bs: int = 64, device=None, opt
     device = torch.device(device) if device is not None else next(model.parameters()).device
     if world is None:
         world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if rank is None:
         rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
     sizes = [dataset.crop_size(i) for i in range(len(dataset))]
     mine = kd.bucket_shard(sizes, world, rank)
     local = eval_records(model, dataset, mine, bs, device, opt_pose=opt_pose, with_loss=criterion is not None)
