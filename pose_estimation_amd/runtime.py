@@ -445,9 +445,9 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
     if GEMM_PANEL and K in (64, 128) and N % 32 == 0 and batch == 1 and lda % 4 == 0 and a_off % 4 == 0:
         wp = ops.gemm_weights_panel(w)
         plan.buffers.append([wp, bias])
-        rows = (M + 127) // 128
+        rows = (M + 255) // 256  # 256-row blocks, one per CU (96 KB of LDS each)
         csplit = 1
-        while rows * csplit < 512 and (N // 32) % (2 * csplit) == 0:  # fill the chip: >= 512 blocks
+        while rows * csplit < 256 and (N // 32) % (2 * csplit) == 0:  # fill the chip: >= 256 blocks
             csplit *= 2
         plan.add("krrn_gemm_panel_x3_f32", P(a.data_ptr() + 4 * a_off), lda, M, K, N, ptr(wp), ptr(bias), ptr(res),
                  ldr, ptr(out), ldo, int(relu), csplit,
