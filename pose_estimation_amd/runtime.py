@@ -410,7 +410,7 @@ BLAS_MAX_WS = 64 << 20
 GEMM_X3 = os.environ.get("KRRN_GEMM_X3", "1") == "1"
 # short-K GEMMs (K = 64 / 128, N % 32 == 0, one row group) on the A-stationary split-bf16 kernel
 # (gemm_panel.hip): the level-0 / level-1 GCN GEMMs, whose 262 MB output makes them write streams
-GEMM_PANEL = os.environ.get("KRRN_GEMM_PANEL", "0") == "1"
+GEMM_PANEL = os.environ.get("KRRN_GEMM_PANEL", "1") == "1"
 GEMM_X3_MINK = int(os.environ.get("KRRN_GEMM_X3_MINK", "256"))
 
 
