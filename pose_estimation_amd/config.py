@@ -18,6 +18,7 @@ The reference loads `config/linemod/lm_v3_1.py`, which is an empty file in the r
 from __future__ import annotations
 
 import copy
+import functools
 import os
 from typing import Any, Dict
 
@@ -98,6 +99,12 @@ LM_OBJLIST = [1, 2, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15]
 SYM_OBJ = [7, 8]  # indices into objlist (eggbox, glue), batchdataset.py:76
 
 
-def models_info() -> Dict[int, Dict[str, float]]:
+@functools.lru_cache(maxsize=1)
+def _models_info() -> Dict[int, Dict[str, float]]:
     with open(os.path.join(CONFIG_DIR, "models_info.yaml")) as f:
         return {int(k): v for k, v in yaml.safe_load(f).items()}
+
+
+def models_info() -> Dict[int, Dict[str, float]]:
+    """models_info.yaml (parsed once per process; a deep copy per call, so callers may edit it)."""
+    return copy.deepcopy(_models_info())

@@ -33,7 +33,7 @@ from . import distributed as kd
 from .dataset import PoseDataset
 from .krrn import KRRN
 from .loss import map_losses
-from .metric import Metric, cal_dis_batch
+from .metric import Metric, add_metric, rt_errors
 from .pose import get_pose
 
 ROT_THR_DEG = 5.0     # trainer.py:156
@@ -58,29 +58,45 @@ def _batches(buckets: Dict[int, List[int]], bs: int):
 def eval_records(model: KRRN, dataset: PoseDataset, indices: Dict[int, List[int]], bs: int, device,
                  opt_pose: bool = True, with_loss: bool = True) -> torch.Tensor:
     """Run the eval path over {S: [crop indices]} in batches of <= bs; returns f64 [n, len(REC)]
-    (rows in the order evaluated)."""
+    (rows in the order evaluated). Every batch's inputs, forward, pose and ADD(-S) are queued on
+    the device without a host round trip; the per-crop records are read back once at the end (the
+    same numbers as a per-batch read-back, without a stall per batch)."""
     metric = Metric(dataset.sym_obj)
-    rows = []
+    pending = []
     for S, idx in _batches(indices, bs):
         data = dataset.batch(idx, device)
         pred = model(data["img_croped"], data["cloud"], data["choose"], data["cls_id"], opt_pose=opt_pose)
         B = len(idx)
-        rec = np.zeros((B, len(REC)), dtype=np.float64)
-        rec[:, _R["crop"]] = idx
-        rec[:, _R["cls"]] = data["cls_id"].reshape(B).cpu().numpy()
-        rec[:, _R["valid"]] = 1.0
+        lc = None
         if with_loss and "xyz" in data and "multi_cls_mask" in data:
-            lc = map_losses(pred, data, per_crop=True).cpu().numpy()  # [B, 8]: xyz, normal, region, mask, counts
-            rec[:, _R["l_xyz"]] = lc[:, 0]
-            rec[:, _R["l_normal"]] = lc[:, 1]
-            rec[:, _R["l_mask"]] = lc[:, 3]
+            lc = map_losses(pred, data, per_crop=True)  # [B, 8]: xyz, normal, region, mask, counts
         base_r, base_t = get_pose(pred, data)
-        a, r, t = cal_dis_batch(metric, base_r, base_t, data)
-        rec[:, _R["add_b"]], rec[:, _R["r_b"]], rec[:, _R["t_b"]] = a, r, t
+        add_b = add_metric(base_r, base_t.reshape(B, 3), data["model_points"], data["target"], data["cls_id"],
+                           metric.sys)
+        add_f = pred_t = None
         if opt_pose:
             # reg = final = (PnP R, TBase t) (trainer.py:198-201)
-            a, r, t = cal_dis_batch(metric, base_r, pred["pred_t"], data)
-            rec[:, _R["add_f"]], rec[:, _R["r_f"]], rec[:, _R["t_f"]] = a, r, t
+            pred_t = pred["pred_t"].reshape(B, 3)
+            add_f = add_metric(base_r, pred_t, data["model_points"], data["target"], data["cls_id"], metric.sys)
+        pending.append((idx, data["cls_id"], data["target_r"], data["target_t"], base_r, base_t, pred_t, add_b, add_f,
+                        lc))
+    rows = []
+    for idx, cls, tr, tt, base_r, base_t, pred_t, add_b, add_f, lc in pending:
+        B = len(idx)
+        rec = np.zeros((B, len(REC)), dtype=np.float64)
+        rec[:, _R["crop"]] = idx
+        rec[:, _R["cls"]] = cls.reshape(B).cpu().numpy()
+        rec[:, _R["valid"]] = 1.0
+        if lc is not None:
+            lcn = lc.cpu().numpy()
+            rec[:, _R["l_xyz"]] = lcn[:, 0]
+            rec[:, _R["l_normal"]] = lcn[:, 1]
+            rec[:, _R["l_mask"]] = lcn[:, 3]
+        rec[:, _R["add_b"]] = add_b.cpu().numpy()
+        rec[:, _R["r_b"]], rec[:, _R["t_b"]] = rt_errors(base_r, base_t, tr, tt)
+        if opt_pose:
+            rec[:, _R["add_f"]] = add_f.cpu().numpy()
+            rec[:, _R["r_f"]], rec[:, _R["t_f"]] = rt_errors(base_r, pred_t, tr, tt)
         rows.append(rec)
     if not rows:
         return torch.zeros((0, len(REC)), dtype=torch.float64)

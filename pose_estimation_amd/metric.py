@@ -112,22 +112,29 @@ class Metric:
         return torch.norm(t1 - t2, dim=-1)
 
 
-def cal_dis_batch(metric: Metric, pred_r: torch.Tensor, pred_t: torch.Tensor, datas):
-    """Trainer.cal_dis (trainer.py:370-381) for every crop of a batch: (ADD(-S) [B], rotation error
-    deg [B], translation error m [B]) as f64 numpy arrays."""
-    dev = pred_t.device
+def rt_errors(pred_r: torch.Tensor, pred_t: torch.Tensor, target_r: torch.Tensor, target_t: torch.Tensor):
+    """(rotation error deg [B], translation error m [B]) as f64 numpy arrays (trainer.py:376-380:
+    metric.angular_distance / translation_distance on the CPU)."""
     B = pred_t.shape[0]
-    add = add_metric(pred_r, pred_t.reshape(B, 3), datas["model_points"], datas["target"], datas["cls_id"],
-                     metric.sys).cpu().numpy()
     R = pred_r.detach().float().cpu().reshape(B, 3, 3)
-    Rt = datas["target_r"].detach().float().cpu().reshape(B, 3, 3)
+    Rt = target_r.detach().float().cpu().reshape(B, 3, 3)
     q1 = torch.nn.functional.normalize(rotation_matrix_to_quaternion(R), p=2.0, dim=-1, eps=1e-12)
     q2 = torch.nn.functional.normalize(rotation_matrix_to_quaternion(Rt), p=2.0, dim=-1, eps=1e-12)
     dot = (q1 * q2).sum(-1)
     eps = 1e-7
     r = (2 * torch.acos(torch.clamp(dot.abs(), -1.0 + eps, 1.0 - eps)) / torch.pi * 180.0).numpy()
-    t = torch.norm(pred_t.detach().float().cpu().reshape(B, 3) - datas["target_t"].detach().float().cpu().reshape(B, 3),
+    t = torch.norm(pred_t.detach().float().cpu().reshape(B, 3) - target_t.detach().float().cpu().reshape(B, 3),
                    dim=-1).double().numpy()
+    return r, t
+
+
+def cal_dis_batch(metric: Metric, pred_r: torch.Tensor, pred_t: torch.Tensor, datas):
+    """Trainer.cal_dis (trainer.py:370-381) for every crop of a batch: (ADD(-S) [B], rotation error
+    deg [B], translation error m [B]) as f64 numpy arrays."""
+    B = pred_t.shape[0]
+    add = add_metric(pred_r, pred_t.reshape(B, 3), datas["model_points"], datas["target"], datas["cls_id"],
+                     metric.sys).cpu().numpy()
+    r, t = rt_errors(pred_r, pred_t, datas["target_r"], datas["target_t"])
     return add, r, t
 
 
