@@ -119,12 +119,26 @@ int krrn_blas_gemm_destroy(krrn_blas_gemm* g);
  * six term products per f32 product): the GCN `feature_map @ weights` of G6/G7
  * (lib/network/point/gcn3d.py:125-127, 184-186) and TBase's Conv1d chain (posenet.py:51-96).
  *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n][k] + bias[n] + res[m*ldr + n])
- * in `batch` strided groups of M rows (a_grp / o_grp / r_grp floats per group). w3f holds W split
+ * in `batch` strided groups of M rows (a_grp / o_grp / r_grp floats per group); ldr = 0 adds one
+ * res row per group (res[g*r_grp + n], a per-crop bias). w3f holds W split
  * into per-wave MFMA fragments (ops.gemm_weights_x3: [N/32][K/8][2][64 lanes][4] u32).
  * K % 32 == 0, N % 128 == 0, lda / ldo / ldr % 4 == 0, 16-byte aligned A / W / out / res. */
 int krrn_gemm_x3_f32(const float* a, int lda, int M, int K, int N, const void* w3f, const float* bias,
                      const float* res, int ldr, float* out, int ldo, int relu, int batch, long long a_grp,
                      long long o_grp, long long r_grp, void* stream);
+
+/* TBase conv2 on a gathered operand (gemm_x3.hip, GA form): conv1 runs by linearity on the fusion's
+ * level rows (posenet.py:51-96 with the concat of lib/network/point/fusion.py:234-238 and the
+ * one-hot channels of lib/network/krrn.py:132-138 folded into two per-crop row tables), and conv2
+ * reads h1 = ReLU(A[b, ia[b, i]] + A2[b, ib[b, i]]) row by row while staging its operand, so h1 is
+ * never materialised (it replaces krrn_gather2_add_f32 + krrn_gemm_x3_f32 on h1):
+ *   out[(b*npts + i)*ldo + n] = act(sum_k h1[b, i, k] W[n][k] + bias[n])
+ * A [B][a_bs floats], rows a_st apart; A2 likewise; ia / ib int32 [B][npts] row indices into the
+ * crop's table. w3f as for krrn_gemm_x3_f32. K % 32 == 0, N % 128 == 0, strides % 4 == 0,
+ * 16-byte aligned tables / W / out, B * a_bs and B * a2_bs < 2^29 floats. */
+int krrn_gemm_x3_gather_f32(const int* ia, const float* A, long long a_bs, int a_st, const int* ib, const float* A2,
+                            long long a2_bs, int a2_st, int npts, int B, int K, int N, const void* w3f,
+                            const float* bias, float* out, int ldo, int relu, void* stream);
 
 /* Short-K GEMM streaming its output (gemm_panel.hip): the fusion's level-0 / level-1 GCN
  * `feature_map @ weights + bias` of Conv_layer (lib/network/point/gcn3d.py:136-164, K = 128,

@@ -81,6 +81,9 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
   // kSU independent loads in flight per thread, then their LDS writes (a rolled load -> write
   // loop would serialise one memory latency per element)
   constexpr int kSU = 8;
+#if KRRN_SMALL_EXP == 2  // timing experiment: no staging loads (LDS left as is)
+  if (total < 0)
+#endif
   for (int e0 = 0; e0 < total; e0 += 256 * kSU) {
     f32x4 v[kSU];
     int dst[kSU];
@@ -161,6 +164,9 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
   f32x4 wr[PF][NW];
 #pragma unroll
   for (int u = 0; u < PF; ++u) wload(s0 + u, wr[u]);
+#if KRRN_SMALL_EXP == 1  // timing experiment: no K loop (staging + epilogue only)
+  if (s1 > 0x7fffffff - 1)
+#endif
   for (int st0 = s0; st0 < s1; st0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -180,7 +186,13 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
-        for (int j = 0; j < NW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w[j][s2], acc[j], 0, 0, 0);
+        for (int j = 0; j < NW; ++j) {
+#if KRRN_SMALL_EXP == 3  // timing experiment: no MFMAs (operands still loaded)
+          acc[j][s2] += av[s2] * w[j][s2];
+#else
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w[j][s2], acc[j], 0, 0, 0);
+#endif
+        }
       c4 += 4;
       if (c4 >= Q) {  // Q >= 4: at most one wrap per step... Q in [1, 4) wraps more
         c4 -= Q;

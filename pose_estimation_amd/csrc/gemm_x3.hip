@@ -25,6 +25,11 @@
 //   * two blocks per CU (68 KB LDS each): one block's barrier / epilogue overlaps the other's
 //     MFMAs; tiles are ordered n-inner and XCD-remapped so a row block's column tiles share an L2
 //     (the A rows are re-read from L2, not HBM).
+//
+// Gathered-A form (GA, krrn_gemm_x3_gather_f32): row m = (crop b, point i) of A is built while it is
+// staged, A[m, k] = relu(P[b, ia[b, i], k] + Q[b, ib[b, i], k]), from two small per-crop row tables —
+// TBase conv1 by linearity (posenet.py: the fusion's level rows times W1, BN / bias / one-hot
+// column folded into them) feeding conv2 directly, so the 1024-wide h1 is never written to HBM.
 #include "krrn_common.h"
 
 namespace {
@@ -41,6 +46,12 @@ constexpr int PX = 3 * KC + 4;  // dwords per LDS row: 12 per 4 k + 4 pad (odd n
 
 struct GemmArgs {
   const float* a;
+  // GA: A[m] = relu(a[b * a_grp + ia[m] * lda] + a2[b * a2_grp + ib[m] * lda2]), b = m / npts
+  const float* a2;
+  const int* ia;
+  const int* ib;
+  long long a2_grp;
+  int lda2, npts;
   const unsigned* w;  // wave fragments [N/32][K/8][2][64][4]
   const float* bias;
   const float* res;
@@ -69,6 +80,7 @@ __device__ __forceinline__ void gx_split(const f32x4 x, gx_u32x4& q0, gx_u32x4& 
 
 __device__ __forceinline__ gx_bf16x8 gx_op(const gx_u32x4 v) { return __builtin_bit_cast(gx_bf16x8, v); }
 
+template <bool GA>
 __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned smem[2 * BM * PX];
 
@@ -82,13 +94,32 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
 
   // activation staging: thread -> rows srow + 64 i (i < 2), 4 k at kq of each chunk
   const int srow = tid >> 2, kq = (tid & 3) * 4;
-  const float* abase = g.a + grp * g.a_grp + (size_t)m0 * g.lda;
+  const float* abase = GA ? g.a : g.a + grp * g.a_grp + (size_t)m0 * g.lda;
   const int rows = min(BM, g.M - m0);
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, ((rows - 1) * g.lda + g.K) * 4, 0x00020000);
-  unsigned aoff[2];
+  // GA: the two row tables are whole buffer resources (bounds checked on the host); rows past M
+  // read 0 through an out-of-range offset
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)abase, (short)0, GA ? (int)(g.a_grp * (g.M / g.npts) * 4) : ((rows - 1) * g.lda + g.K) * 4, 0x00020000);
+  __amdgpu_buffer_rsrc_t rsA2;
+  unsigned aoff[2], aoff2[2];
+  if constexpr (GA) {
+    rsA2 = __builtin_amdgcn_make_buffer_rsrc((void*)g.a2, (short)0, (int)(g.a2_grp * (g.M / g.npts) * 4),
+                                             0x00020000);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) aoff[i] = (unsigned)(((srow + 64 * i) * g.lda + kq) * 4);
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + srow + 64 * i;
+      if (m < g.M) {
+        const int b = m / g.npts;
+        aoff[i] = (unsigned)((b * g.a_grp + (long long)g.ia[m] * g.lda + kq) * 4);
+        aoff2[i] = (unsigned)((b * g.a2_grp + (long long)g.ib[m] * g.lda2 + kq) * 4);
+      } else {
+        aoff[i] = aoff2[i] = 0x80000000u;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i] = (unsigned)(((srow + 64 * i) * g.lda + kq) * 4);
+  }
 
   const int G = g.K >> 3;  // 8-k groups
   const unsigned* wb = g.w + ((size_t)((n0 >> 5) + wave) * G) * 512 + lane * 4;
@@ -99,19 +130,30 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
   // + K <= lda) ends inside the tensor
   const int nch = g.K / KC;  // even (K % 32 == 0)
   f32x4 ra[2][2];  // A chunks c + 1 and c + 2 in flight (2 float4 per thread per chunk)
+  f32x4 rq[GA ? 2 : 1][2];  // GA: the second table's rows
   auto load_a = [&](int c, int s) {
     c = min(c, nch - 1);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
       ra[s][i] = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, aoff[i] + (unsigned)(c * KC * 4), 0, 0));
+      if constexpr (GA)
+        rq[s][i] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA2, aoff2[i] + (unsigned)(c * KC * 4), 0, 0));
+    }
   };
   auto store_a = [&](int s) {
     unsigned* d = smem + s * BM * PX;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       gx_u32x4 q0, q1, q2;
-      gx_split(ra[s][i], q0, q1, q2);
+      f32x4 x = ra[s][i];
+      if constexpr (GA) {
+        x += rq[s][i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
+      }
+      gx_split(x, q0, q1, q2);
       unsigned* p = d + (srow + 64 * i) * PX + 3 * kq;
       *reinterpret_cast<gx_u32x4*>(p) = q0;
       *reinterpret_cast<gx_u32x4*>(p + 4) = q1;
@@ -202,7 +244,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(const GemmArgs g) {
   const int n = n0 + wave * 32 + frow;
   const float bi = g.bias ? g.bias[n] : 0.f;
   float* ob = g.out + grp * g.o_grp + n;
-  const float* rb = g.res ? g.res + grp * g.r_grp + n : nullptr;
+  const float* rb = g.res ? g.res + grp * g.r_grp + n : nullptr;  // ldr = 0: one row per group
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -225,16 +267,43 @@ KRRN_API int krrn_gemm_x3_f32(const float* a, int lda, int M, int K, int N, cons
   if (M < 1 || K < KC || N < BN || batch < 1) return KRRN_ESHAPE;
   if ((K % (2 * KC)) || (N % BN) || lda < K || ldo < N) return KRRN_ESHAPE;
   if ((lda & 3) || (ldo & 3) || (a_grp & 3) || (o_grp & 3)) return KRRN_EALIGN;
-  if (res && (ldr < N || (r_grp & 3))) return KRRN_ESHAPE;
+  if (res && ((ldr != 0 && ldr < N) || (r_grp & 3))) return KRRN_ESHAPE;
   if (!krrn_aligned16(a) || !krrn_aligned16(w3f) || !krrn_aligned16(out)) return KRRN_EALIGN;
   if ((long long)BM * lda * 4 >= 0x7FFFFFFFLL) return KRRN_ESHAPE;  // 32-bit buffer offsets
   const long long tiles = (long long)krrn_cdiv(M, BM) * (N / BN) * batch;
   if (tiles > 0x7FFFFFFFLL) return KRRN_ESHAPE;
   GemmArgs g;
-  g.a = a; g.w = reinterpret_cast<const unsigned*>(w3f); g.bias = bias; g.res = res; g.out = out;
+  g.a = a; g.a2 = nullptr; g.ia = g.ib = nullptr; g.a2_grp = 0; g.lda2 = 0; g.npts = 1;
+  g.w = reinterpret_cast<const unsigned*>(w3f); g.bias = bias; g.res = res; g.out = out;
   g.lda = lda; g.M = M; g.K = K; g.N = N; g.ldr = ldr; g.ldo = ldo; g.relu = relu;
   g.a_grp = a_grp; g.o_grp = o_grp; g.r_grp = r_grp;
   g.mt = krrn_cdiv(M, BM); g.nt = N / BN; g.total = (int)tiles;
-  hipLaunchKernelGGL(gemm_x3_kernel, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, g);
+  hipLaunchKernelGGL(gemm_x3_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, g);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_gemm_x3_gather_f32(const int* ia, const float* A, long long a_bs, int a_st, const int* ib,
+                                     const float* A2, long long a2_bs, int a2_st, int npts, int B, int K, int N,
+                                     const void* w3f, const float* bias, float* out, int ldo, int relu,
+                                     void* stream) {
+  if (!ia || !A || !ib || !A2 || !w3f || !out) return KRRN_EARG;
+  if (npts < 1 || B < 1 || K < KC || N < BN) return KRRN_ESHAPE;
+  if ((K % (2 * KC)) || (N % BN) || a_st < K || a2_st < K || ldo < N) return KRRN_ESHAPE;
+  if ((a_st & 3) || (a2_st & 3) || (a_bs & 3) || (a2_bs & 3) || (ldo & 3)) return KRRN_EALIGN;
+  if (!krrn_aligned16(A) || !krrn_aligned16(A2) || !krrn_aligned16(w3f) || !krrn_aligned16(out)) return KRRN_EALIGN;
+  // 32-bit buffer offsets over the whole row tables; the kernel trusts ia / ib to index rows of
+  // their crop's table (a_bs / a_st floats), as krrn_gather2_add_f32 does
+  if ((long long)B * a_bs * 4 >= 0x7FFFFFFFLL || (long long)B * a2_bs * 4 >= 0x7FFFFFFFLL) return KRRN_ESHAPE;
+  const long long M = (long long)B * npts;
+  const long long tiles = (long long)krrn_cdiv(M, BM) * (N / BN);
+  if (M > 0x7FFFFFFFLL || tiles > 0x7FFFFFFFLL) return KRRN_ESHAPE;
+  GemmArgs g;
+  g.a = A; g.a2 = A2; g.ia = ia; g.ib = ib; g.a_grp = a_bs; g.a2_grp = a2_bs; g.lda = a_st; g.lda2 = a2_st;
+  g.npts = npts;
+  g.w = reinterpret_cast<const unsigned*>(w3f); g.bias = bias; g.res = nullptr; g.out = out;
+  g.M = (int)M; g.K = K; g.N = N; g.ldr = 0; g.ldo = ldo; g.relu = relu;
+  g.o_grp = 0; g.r_grp = 0;
+  g.mt = krrn_cdiv(g.M, BM); g.nt = N / BN; g.total = (int)tiles;
+  hipLaunchKernelGGL(gemm_x3_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, g);
   return krrn_launch_status();
 }

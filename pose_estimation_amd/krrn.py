@@ -176,7 +176,8 @@ class KRRNPlan:
             def emit_tb_l1(fb):
                 plan.fork([tb_sid])
                 with plan.on_stream(tb_sid):
-                    tb_pre.update(emit_tbase_level1(model.pose.t_net, plan, B, N, N1, fb["feat1"], fb["feat2"]))
+                    tb_pre.update(emit_tbase_level1(model.pose.t_net, plan, B, N, N1, fb["feat1"], fb["feat2"],
+                                                      cls_key="cls", inc_r=cfg.Module.POSENet.INC_R, num_cls=C))
 
             if TBASE_EARLY:
                 hooks["level1"].append(tracked(emit_tb_l1))

@@ -12,6 +12,7 @@ conv4 + the mean over points is one reduction launch per crop.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -19,6 +20,11 @@ import torch.nn as nn
 
 from . import ops
 from .runtime import Late, Plan, add_conv, add_gemm, ptr
+
+
+# conv2 gathers h1 = ReLU(P1[nn1] + P2[nn2]) inside its operand staging (krrn_gemm_x3_gather_f32)
+# instead of a separate gather-add launch writing the 262 MB h1 (KRRN_TBASE_GATHER=0: the old form)
+TBASE_GATHER = os.environ.get("KRRN_TBASE_GATHER", "1") == "1"
 
 
 class TBase(nn.Module):
@@ -42,14 +48,47 @@ class PoseNet(nn.Module):
         self.t_net = TBase(cfg)
 
 
+def _conv1_fold(tb: TBase, inc_r: int, num_cls: int, dev):
+    """conv1 + bn1 folded: (W1 [1024, inc_r + C], spec1 with the BN scale / bias, colv [C, 1024] =
+    the one-hot columns pre-multiplied by the BN scale)."""
+    w1 = tb.conv1.weight.detach()[:, :, 0]
+    spec1 = ops.make_linear(w1[:, :inc_r], tb.conv1.bias, tb.bn1, dev)
+    np1 = ops.pad4(1024)
+    colv = torch.zeros(num_cls, np1, device=dev)
+    colv[:, :1024] = (spec1.scale[:1024, None] * w1[:, inc_r:inc_r + num_cls].to(dev).float()).t()
+    return w1, spec1, colv
+
+
 def emit_tbase_level1(tb: TBase, plan: Plan, B: int, N: int, N1: int, feat1: torch.Tensor,
-                      feat2: torch.Tensor) -> dict:
+                      feat2: torch.Tensor, cls_key: str = "cls", inc_r: int = 1280, num_cls: int = 1) -> dict:
     """The part of TBase conv1 (by linearity, see build_tbase_plan) that needs only the level-0 /
     level-1 features: P1 = feat1[:N1] W1[:, 512:896]^T + feat2 W1[:, 896:1280]^T, on the plan's
-    current stream. Emitted from the fusion's 'level1' hook, it runs beside the level-2 GCN chain."""
+    current stream. Emitted from the fusion's 'level1' hook, it runs beside the level-2 GCN chain.
+    With TBASE_GATHER the BN scale is folded into those weights and the BN shift + conv1 bias + the
+    crop's one-hot column are added here, so conv2 only has to gather, add and ReLU (fused into its
+    operand staging, krrn_gemm_x3_gather_f32)."""
     dev = plan.device
-    w1 = tb.conv1.weight.detach()[:, :, 0]
     np1 = ops.pad4(1024)
+    if TBASE_GATHER:
+        w1, spec1, colv = _conv1_fold(tb, inc_r, num_cls, dev)
+        wb = ops.make_linear(w1[:, 512:896], None, None, dev)
+        wc = ops.make_linear(w1[:, 896:1280], None, None, dev)
+        b2 = plan.buf((B, np1))
+        plan.add("krrn_gather_rows_f32", Late(cls_key), 1, 1, 1, ptr(colv), 0, np1, ptr(b2), np1, np1, np1, B)
+        Q = plan.buf((B * N1, np1))
+        P1 = plan.buf((B * N1, np1))
+        # Q = s (feat2 Wc) + shift + b2[crop] (the crop's row of b2 broadcast: ldr = 0, one row per group)
+        ok = add_gemm(plan, a=feat2, a_off=0, lda=384, M=N1, wt=wc.wt[0], K=wc.cin_p, N=np1, scale=spec1.scale,
+                      bias=spec1.bias, out=Q, ldo=np1, relu=False, res=b2, ldr=0, batch=B, a_grp=N1 * 384,
+                      o_grp=N1 * np1, r_grp=np1, cin=wc.cin, cout=wc.cout, tag="tbase_gemm", require_x3=True) and \
+            add_gemm(plan, a=feat1, a_off=0, lda=384, M=N1, wt=wb.wt[0], K=wb.cin_p, N=np1, scale=spec1.scale,
+                     bias=None, out=P1, ldo=np1, relu=False, res=Q, ldr=np1, batch=B, a_grp=N * 384,
+                     o_grp=N1 * np1, r_grp=N1 * np1, cin=wb.cin, cout=wb.cout, tag="tbase_gemm", require_x3=True)
+        if not ok:
+            raise RuntimeError("TBase gathered conv2 needs the split-bf16 GEMM (KRRN_GEMM_X3=1)")
+        plan.buffers.append([wb, wc, spec1, colv])
+        return dict(P1=P1, Q=Q, b2=b2, folded=True)
+    w1 = tb.conv1.weight.detach()[:, :, 0]
     wb = ops.make_linear(w1[:, 512:896], None, None, dev)
     wc = ops.make_linear(w1[:, 896:1280], None, None, dev)
     Q = plan.buf((B * N1, np1))
@@ -87,24 +126,23 @@ def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, 
     launch applies BN + one-hot column + ReLU per point. 29 instead of 168 GFLOP at config 2.
     `pre`: P1 already emitted by emit_tbase_level1 on stream `pre_sid` (joined here before use)."""
     dev = plan.device
-    w1 = tb.conv1.weight.detach()[:, :, 0]
-    spec1 = ops.make_linear(w1[:, :inc_r], tb.conv1.bias, tb.bn1, dev)
     # one-hot columns, pre-multiplied by the folded BN scale: colv[c] = scale * W1[:, inc_r + c]
+    w1, spec1, colv = _conv1_fold(tb, inc_r, num_cls, dev)
     np1 = ops.pad4(1024)
-    colv = torch.zeros(num_cls, np1, device=dev)
-    colv[:, :1024] = (spec1.scale[:1024, None] * w1[:, inc_r:inc_r + num_cls].to(dev).float()).t()
     spec2 = ops.make_linear(tb.conv2.weight, tb.conv2.bias, tb.bn2, dev)
     spec3 = ops.make_linear(tb.conv3.weight, tb.conv3.bias, tb.bn3, dev)
     w4 = tb.conv4.weight.detach()[:3, :, 0].float().contiguous().to(dev)
     b4 = tb.conv4.bias.detach()[:3].float().contiguous().to(dev)
-    b2 = plan.buf((B, np1))
-    h1 = plan.buf((B * N, 1024))
+    gathered = levels is not None and TBASE_GATHER
+    h1 = None if gathered else plan.buf((B * N, 1024))
     h2 = plan.buf((B * N, 256))
     h3 = plan.buf((B * N, 256))
     pred_t = plan.buf((B, 3))
     M = B * N
-    plan.add("krrn_gather_rows_f32", Late(cls_key), 1, 1, 1, ptr(colv), 0, np1, ptr(b2), np1, np1, np1, B)
     keep = [spec1, spec2, spec3, colv, w4, b4]
+    if not gathered:
+        b2 = plan.buf((B, np1))
+        plan.add("krrn_gather_rows_f32", Late(cls_key), 1, 1, 1, ptr(colv), 0, np1, ptr(b2), np1, np1, np1, B)
 
     def gemm(a, K, spec, out, bias2=None, rows=M, relu=True):
         np_ = ops.pad4(spec.cout)
@@ -124,15 +162,35 @@ def build_tbase_plan(tb: TBase, plan: Plan, B: int, N: int, feat: torch.Tensor, 
         wa = ops.make_linear(w1[:, 0:512], None, None, dev)
         keep += [wa]
         P2 = plan.buf((B * N2, np1))
-        gemm(levels["fm5"], 512, wa, P2, rows=B * N2, relu=False)
+        if gathered:  # BN scale folded into W1's columns, as for P1 (emit_tbase_level1)
+            if not add_gemm(plan, a=levels["fm5"], a_off=0, lda=512, M=B * N2, wt=wa.wt[0], K=wa.cin_p, N=np1,
+                            scale=spec1.scale, bias=None, out=P2, ldo=np1, relu=False, cin=wa.cin, cout=wa.cout,
+                            tag="tbase_gemm", require_x3=True):
+                raise RuntimeError("TBase gathered conv2 needs the split-bf16 GEMM (KRRN_GEMM_X3=1)")
+        else:
+            gemm(levels["fm5"], 512, wa, P2, rows=B * N2, relu=False)
         if pre is None:
-            pre = emit_tbase_level1(tb, plan, B, N, N1, levels["feat1"], levels["feat2"])
+            pre = emit_tbase_level1(tb, plan, B, N, N1, levels["feat1"], levels["feat2"], cls_key=cls_key,
+                                    inc_r=inc_r, num_cls=num_cls)
         else:
             plan.join([pre_sid])
         P1 = pre["P1"]
-        plan.add("krrn_gather2_add_f32", ptr(levels["nn2"]), ptr(P2), N2 * np1, np1, ptr(levels["nn1"]), ptr(P1),
-                 N1 * np1, np1, N, np1, ptr(spec1.scale), ptr(spec1.bias), ptr(b2), 1, ptr(h1), N * 1024, 1024, B)
-    gemm(h1, 1024, spec2, h2)
+        if gathered:
+            # conv2 with h1 = ReLU(P1[nn1] + P2[nn2]) built in its operand staging (never in HBM)
+            w2 = tb.conv2.weight.detach()[:, :, 0].to(dev).float() * spec2.scale[:256].reshape(256, 1)
+            w3 = ops.gemm_weights_x3(w2.contiguous())
+            keep += [w3]
+            plan.add("krrn_gemm_x3_gather_f32", ptr(levels["nn1"]), ptr(P1), N1 * np1, np1, ptr(levels["nn2"]),
+                     ptr(P2), N2 * np1, np1, N, B, 1024, 256, ptr(w3), ptr(spec2.bias), ptr(h2), 256, 1,
+                     meta=dict(kernel="gemm_x3", flops=2.0 * 1024 * 256 * M, tag="tbase_gemm", M=M, N=256, K=1024,
+                               splits=1, mfma_flops=2.0 * M * 256 * 1024 * 6 / 16,
+                               mfma_bf16_flops=2.0 * M * 256 * 1024 * 6))
+        else:
+            plan.add("krrn_gather2_add_f32", ptr(levels["nn2"]), ptr(P2), N2 * np1, np1, ptr(levels["nn1"]),
+                     ptr(P1), N1 * np1, np1, N, np1, ptr(spec1.scale), ptr(spec1.bias), ptr(b2), 1, ptr(h1),
+                     N * 1024, 1024, B)
+    if not gathered:
+        gemm(h1, 1024, spec2, h2)
     gemm(h2, 256, spec3, h3)
     plan.add("krrn_tbase_tail_f32", ptr(h3), B, N, 256, ptr(w4), ptr(b4), Late(cloud_key), ptr(pred_t), ptr(None))
     plan.buffers.append(keep)

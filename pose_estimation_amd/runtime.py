@@ -57,6 +57,7 @@ _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])
 _lib.register("krrn_gemm_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, L, L, L, P])
+_lib.register("krrn_gemm_x3_gather_f32", [P, P, L, I, P, P, L, I, I, I, I, I, P, P, P, I, I, P])
 _lib.register("krrn_gemm_panel_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, P])
 
 
@@ -128,6 +129,12 @@ class Sync:
         streams[self.dst].wait_event(self.event)
 
 
+# KRRN_DIAG_DROP=name[,name...]: leave every launch of those C-ABI entry points out of new plans.
+# A what-if timing diagnostic (profiles/whatif.sh: how much the step shrinks if a kernel family
+# were free); the outputs are meaningless with it set, and nothing in the package sets it.
+_DIAG_DROP = frozenset(filter(None, os.environ.get("KRRN_DIAG_DROP", "").split(",")))
+
+
 class Plan:
     """An ordered launch list plus the workspaces it owns.
 
@@ -168,6 +175,8 @@ class Plan:
         return ws
 
     def add(self, name: str, *args, meta: Optional[dict] = None):
+        if _DIAG_DROP and name in _DIAG_DROP:
+            return  # what-if timing diagnostic only (results are wrong): see _DIAG_DROP
         self.ops.append(Op(name, list(args) + [Late(_skey(self.cur))], meta, self.cur))
 
     @contextmanager
@@ -431,18 +440,20 @@ class _BlasPlan:
 def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: torch.Tensor, K: int, N: int,
              scale: Optional[torch.Tensor], bias: Optional[torch.Tensor], out: torch.Tensor, ldo: int, relu: bool,
              res: Optional[torch.Tensor] = None, ldr: int = 0, batch: int = 1, a_grp: int = 0, o_grp: int = 0,
-             r_grp: int = 0, cin: Optional[int] = None, cout: Optional[int] = None, tag: str = "gemm") -> bool:
+             r_grp: int = 0, cin: Optional[int] = None, cout: Optional[int] = None, tag: str = "gemm",
+             require_x3: bool = False) -> bool:
     """Append a plain GEMM out[m, n] = act(scale[n] * (A[m] . wt[n]) + bias[n] (+ res[m, n])) on hipBLASLt
     (krrn_blas_gemm_*; scale folded into the weights). Returns False when hipBLASLt is disabled
     (KRRN_BLAS=0) or rejects the problem: the caller then emits its own kernel. Short-K GEMMs go to
-    the A-stationary split-bf16 kernel and K >= 256 ones to gemm_x3 first (own kernels)."""
+    the A-stationary split-bf16 kernel and K >= 256 ones to gemm_x3 first (own kernels).
+    require_x3: only gemm_x3 will do (its ldr = 0 per-group row broadcast); False if ineligible."""
     dev = plan.device
     w = wt.reshape(N, -1)[:, :K].float()
     if scale is not None:
         w = w * scale.reshape(N, 1).to(w.device)
     w = w.contiguous()
     flops = 2.0 * (cin or K) * (cout or N) * M * batch
-    if GEMM_PANEL and K in (64, 128) and N % 32 == 0 and batch == 1 and lda % 4 == 0 and a_off % 4 == 0:
+    if GEMM_PANEL and not require_x3 and K in (64, 128) and N % 32 == 0 and batch == 1 and lda % 4 == 0 and a_off % 4 == 0:
         wp = ops.gemm_weights_panel(w)
         plan.buffers.append([wp, bias])
         rows = (M + 255) // 256  # 256-row blocks, one per CU (96 KB of LDS each)
@@ -465,7 +476,7 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
                  meta=dict(kernel="gemm_x3", flops=flops, tag=tag, M=M * batch, N=N, K=K, splits=1,
                            mfma_flops=2.0 * M * batch * N * K * 6 / 16, mfma_bf16_flops=2.0 * M * batch * N * K * 6))
         return True
-    if not BLAS:
+    if not BLAS or require_x3:
         return False
     h = ctypes.c_void_p()
     wsb = ctypes.c_longlong()

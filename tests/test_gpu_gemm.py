@@ -130,3 +130,50 @@ def test_gemm_panel_rejects(dev):
     assert L.krrn_gemm_panel_x3_f32(P(A.data_ptr() + 4), 128, 64, 128, 128, ptr(wp), P(0), P(0), 0, ptr(out), 128, 0,
                                     1, s) < 0
     assert L.krrn_gemm_panel_x3_f32(P(0), 128, 64, 128, 128, ptr(wp), P(0), P(0), 0, ptr(out), 128, 0, 1, s) < 0
+
+
+def test_gemm_x3_group_row_bias(dev):
+    """ldr = 0: one res row per group, added to every row of the group (TBase's per-crop one-hot
+    column + BN shift folded into conv1's level rows, posenet.emit_tbase_level1)."""
+    g = torch.Generator().manual_seed(11)
+    B, M, K, N = 4, 250, 384, 256
+    A = torch.randn(B, M, K, generator=g).to(dev)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(dev)
+    b2 = torch.randn(B, N, generator=g).to(dev)
+    out = torch.zeros(B, M, N, device=dev)
+    _run(A, 0, K, M, K, N, W, None, b2, 0, out, N, False, batch=B, a_grp=M * K, o_grp=M * N, r_grp=N)
+    ref = torch.einsum("bmk,nk->bmn", A.double(), W.double()) + b2.double()[:, None, :]
+    assert float((out.double() - ref).abs().max()) <= 2e-6 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("B,npts,n1,n2", [(3, 300, 75, 18), (2, 1000, 250, 62), (1, 130, 40, 10)])
+def test_gemm_x3_gather_vs_torch(dev, B, npts, n1, n2):
+    """krrn_gemm_x3_gather_f32: TBase conv2 on h1 = ReLU(P1[b, ia] + P2[b, ib]) gathered while the
+    operand is staged (posenet.py:51-96 by linearity) vs torch on the materialised h1."""
+    g = torch.Generator().manual_seed(npts + n1)
+    K, N = 1024, 256
+    P1 = torch.randn(B, n1, K, generator=g).to(dev)
+    P2 = torch.randn(B, n2, K, generator=g).to(dev)
+    ia = torch.randint(0, n1, (B, npts), generator=g, dtype=torch.int32).to(dev)
+    ib = torch.randint(0, n2, (B, npts), generator=g, dtype=torch.int32).to(dev)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(dev)
+    bias = (0.1 * torch.randn(N, generator=g)).to(dev)
+    out = torch.full((B * npts, N + 4), 7.0, device=dev)
+    w3 = ops.gemm_weights_x3(W)
+    st = _lib.lib().krrn_gemm_x3_gather_f32(ptr(ia), ptr(P1), n1 * K, K, ptr(ib), ptr(P2), n2 * K, K, npts, B, K, N,
+                                           ptr(w3), ptr(bias), ptr(out), N + 4, 1,
+                                           P(torch.cuda.current_stream().cuda_stream))
+    _lib.check(st, "gemm_x3_gather")
+    torch.cuda.synchronize()
+    bi = torch.arange(B, device=dev)[:, None]
+    h1 = (P1[bi, ia.long()] + P2[bi, ib.long()]).clamp_min(0).reshape(B * npts, K)
+    ref64 = (h1.double() @ W.double().t() + bias.double()).clamp_min(0)
+    ref32 = (h1 @ W.t() + bias).clamp_min(0)
+    err = float((out[:, :N].double() - ref64).abs().max())
+    err32 = float((ref32.double() - ref64).abs().max())
+    assert err <= max(4 * err32, 2e-6 * float(ref64.abs().max())), (err, err32)
+    assert torch.all(out[:, N:] == 7.0), "wrote past N"
+    # identical to the non-gathered kernel on the materialised h1 (same staging arithmetic)
+    out2 = torch.zeros(B * npts, N, device=dev)
+    _run(h1.contiguous(), 0, K, B * npts, K, N, W, bias, None, 0, out2, N, True)
+    assert torch.equal(out[:, :N], out2)
