@@ -140,6 +140,17 @@ int krrn_gemm_x3_gather_f32(const int* ia, const float* A, long long a_bs, int a
                             long long a2_bs, int a2_st, int npts, int B, int K, int N, const void* w3f,
                             const float* bias, float* out, int ldo, int relu, void* stream);
 
+/* One HRNet BasicBlock without downsample (conv_bb.hip; lib/network/hrnet/myhrnet.py:34-63):
+ *   out = ReLU(s2 * conv3x3(ReLU(s1 * conv3x3(in) + b1)) + b2 + in)
+ * on NHWC rows (channel stride / offset in_cs / in_co, out_cs / out_co; C padded channels, a
+ * multiple of 4, pad channels zero), both convs stride 1 / pad 1 on the bf16 matrix cores at f32
+ * accuracy (split operands), the intermediate kept in LDS. w1 / w2: ops.bb_weights_x3 planes;
+ * s / b: [C] eval-BN scale / bias (16-byte aligned). T output rows per block (ops.bb_tile_rows);
+ * in and out must not alias. */
+int krrn_basic_block_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int C, const void* w1,
+                            const float* s1, const float* b1, const void* w2, const float* s2, const float* b2,
+                            float* out, int out_cs, int out_co, int T, void* stream);
+
 /* Short-K GEMM streaming its output (gemm_panel.hip): the fusion's level-0 / level-1 GCN
  * `feature_map @ weights + bias` of Conv_layer (lib/network/point/gcn3d.py:136-164, K = 128,
  * N = 8 * 128) and layer1's 64 -> 256 1x1 convs (myhrnet.py:65-103, K = 64):

@@ -286,6 +286,41 @@ def gemm_weights_x3(wt: torch.Tensor) -> torch.Tensor:
     return c.permute(0, 2, 4, 3, 1, 5).contiguous()                 # nb g q fh nl 4
 
 
+def bb_weights_x3(wt: torch.Tensor, C: int) -> torch.Tensor:
+    """A BasicBlock conv's weights [N >= C][9 C] f32 (k = tap * C + c, ops.make_conv's packing) ->
+    the split planes krrn_basic_block_x3_f32 reads, int32: the [m h] plane [NTt*16][KQp][4]
+    (per output channel and channel quad kq: m0..m3 h0..h3 bf16) then the [l] plane [NTt*16][KQp][2]
+    (l0..l3); NTt = ceil(C / 16) channel tiles, KQp = 9 C / 4 rounded up to a multiple of 16 (the
+    kernel runs its reduction in groups of 4 steps of 4 quads), zero padded (padding channels /
+    quads contribute exact zeros)."""
+    ntt = (C + 15) // 16
+    kqp = -(-(9 * C // 4) // 16) * 16
+    w = torch.zeros(ntt * 16, kqp * 4, dtype=torch.float32, device=wt.device)
+    n = min(wt.shape[0], C)
+    w[:n, :9 * C] = wt.reshape(wt.shape[0], -1)[:n, :9 * C].float()
+    h, m, l = (t.reshape(ntt * 16, kqp, 4) for t in split_bf16x3(w))
+    mh = torch.cat([m, h], dim=-1).contiguous().view(torch.int32).reshape(-1)
+    lp = l.contiguous().view(torch.int32).reshape(-1)
+    return torch.cat([mh, lp]).contiguous()
+
+
+def bb_tile_rows(B: int, H: int, W: int, C: int, max_lds: int = 160 * 1024) -> int:
+    """Output rows per block of krrn_basic_block_x3_f32: the T minimising the per-CU pixel-tile
+    work ceil(blocks / 256) * (conv1 + conv2 16-pixel tiles of a block), LDS within max_lds
+    (mirror of the kernel's bb_lds_bytes); ties -> larger T (fewer halo rows staged). 0 = none fits."""
+    qp = (C // 4) | 1
+    best, best_t = None, 0
+    for T in range(1, H + 1):
+        lds = 2 * (min(T + 4, H + 2) + min(T + 2, H + 2)) * (W + 2) * qp * 16
+        if lds > max_lds:
+            continue
+        blocks = B * (-(-H // T))
+        cost = -(-blocks // 256) * (-(-(min(T + 2, H) * W) // 16) + -(-(T * W) // 16)) + 2
+        if best is None or cost <= best:
+            best, best_t = cost, T
+    return best_t
+
+
 def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:
     """GEMM weights [N][K] f32 (scale folded) -> the wave fragments krrn_gemm_panel_x3_f32 reads: int32
     [N/32][K/8][3][64][4]. Fragment (column tile nb, 8-k group g, quad q) is one coalesced 1-KB wave
