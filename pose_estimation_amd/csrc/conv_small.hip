@@ -17,7 +17,9 @@
 // the CUs. Per (tap, 16-channel group): lane (pixel m = l % 16, quad g = l / 16) reads the 4
 // channels 4g..4g+3 of its input pixel from LDS (one ds_read_b128 feeds 4 MFMAs: MFMA s sums
 // k = 4g + s over the 4 lane groups) and the matching weight quad of output channel n = l % 16
-// straight from global memory (the weights are read by every block: L2-resident).
+// straight from global memory (the weights are read by every block: L2-resident). The weights are
+// the MFMA's first operand, so each lane ends with 4 consecutive channels of one pixel: the
+// epilogue (BN, residual, ReLU) is one float4 load / store per lane and channel tile.
 //
 // Numerics: f32 operands, f32 accumulation (v_mfma_f32_16x16x4_f32 is an fma chain); the k order
 // differs from the implicit-GEMM kernel's, so results agree with it to f32 rounding.
@@ -190,7 +192,9 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
 #if KRRN_SMALL_EXP == 3  // timing experiment: no MFMAs (operands still loaded)
           acc[j][s2] += av[s2] * w[j][s2];
 #else
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s2], w[j][s2], acc[j], 0, 0, 0);
+          // weights as the first operand (rows = output channels), pixels as the second: lane l's
+          // accumulator is channels 4 (l / 16) .. +3 of pixel l % 16 (one float4 in the epilogue)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j][s2], av[s2], acc[j], 0, 0, 0);
 #endif
         }
       c4 += 4;
@@ -222,22 +226,22 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
     }
   }
 
-  // ---- epilogue: acc[j][i] = (pixel 16 mi + 4g + i, channel n0 + 16j + fr) --------------------
+  // ---- epilogue: acc[j][i] = (channel n0 + 16j + 4g + i, pixel 16 mi + fr): float4 per lane ------
+  const int mo = p0 + 16 * mi + fr;
+  if (mo >= a.M) return;
 #pragma unroll
   for (int j = 0; j < NW; ++j) {
-    const int n = n0 + 16 * j + fr;
-    if (n >= a.n_store) continue;
-    const float sc = a.scale ? a.scale[n] : 1.f;
-    const float bi = a.bias ? a.bias[n] : 0.f;
+    const int n = n0 + 16 * j + 4 * g;
+    if (n >= a.n_store) continue;  // n_store is a multiple of 4
+    const f32x4 sc = a.scale ? *reinterpret_cast<const f32x4*>(a.scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 v = acc[j] * sc + bi;
+    if (a.res) v += *reinterpret_cast<const f32x4*>(a.res + (size_t)mo * a.res_cs + a.res_co + n);
+    if (a.relu) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int mo = p0 + 16 * mi + 4 * g + i;
-      if (mo >= a.M) continue;
-      float v = acc[j][i] * sc + bi;
-      if (a.res) v += a.res[(size_t)mo * a.res_cs + a.res_co + n];
-      if (a.relu) v = fmaxf(v, 0.f);
-      a.out[(size_t)mo * a.out_cs + a.out_co + n] = v;
+      for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
     }
+    *reinterpret_cast<f32x4*>(a.out + (size_t)mo * a.out_cs + a.out_co + n) = v;
   }
 }
 
@@ -334,6 +338,10 @@ int make_args(const float* in, int in_cs, int in_co, int B, int H, int W, int ci
   if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
   if (!krrn_aligned16(in) || !krrn_aligned16(wt)) return KRRN_EALIGN;
   if (out_co + n_store > out_cs || (res && res_co + n_store > res_cs)) return KRRN_ESHAPE;
+  // the epilogue stores / loads float4 channel quads
+  if ((n_store & 3) || (out_cs & 3) || (out_co & 3) || !krrn_aligned16(out)) return KRRN_EALIGN;
+  if (res && ((res_cs & 3) || (res_co & 3) || !krrn_aligned16(res))) return KRRN_EALIGN;
+  if ((scale && !krrn_aligned16(scale)) || (bias && !krrn_aligned16(bias))) return KRRN_EALIGN;
   if (nw < 1 || nw > 3 || (ks != 1 && ks != 2 && ks != 4)) return KRRN_EARG;
   if ((ksize != 1 && ksize != 3) || (stride != 1 && stride != 2)) return KRRN_EARG;
   const int pad = (ksize - 1) / 2;
