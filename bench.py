@@ -3,11 +3,10 @@
 A step = one pass of the hot path over one batch of synthetic LineMOD crops resident in HBM:
 HRNet-W18 + heads + class select/normalise + choose gather + FusionNetLite + TBase (pred_t)
 + batched PnP-RANSAC (R), including the device-side randomness (pool permutations, the 256-
-point PnP subset, RANSAC hypotheses). By default the step is a two-stage software pipeline over
-two batch slots (pipeline.PipelinedPipeline, split after the heads): stage A = backbone + heads of
-batch k+1 and stage B = fusion + TBase + PnP of batch k replay as two hipGraphs on two streams, so
-every step completes one whole batch (the latency-bound tail overlaps MFMA-bound convs);
---pipeline none runs one batch end to end as one hipGraph. With --gpus N
+point PnP subset, RANSAC hypotheses). The step is one hipGraph replay of the whole path (the plan's
+independent branches as graph branches, runtime.Plan); the two-slot pipeline (--pipeline
+heads|backbone|pose) and concurrent micro-batches overlap only with KRRN_STREAMS=1, which is not
+reproducible on this stack and measured no faster. With --gpus N
 (torchrun, one process per GPU, RCCL) every rank runs its own batch (weak scaling) and the
 per-crop pose records are all-gathered over RCCL after every step.
 
@@ -34,6 +33,7 @@ from pose_estimation_amd import distributed as kd  # noqa: E402
 from pose_estimation_amd.config import make_config  # noqa: E402
 from pose_estimation_amd.krrn import KRRN  # noqa: E402
 from pose_estimation_amd.pipeline import BatchPipeline, PipelinedPipeline  # noqa: E402
+from pose_estimation_amd.runtime import PLAN_STREAMS, STREAMS  # noqa: E402
 from pose_estimation_amd.synthetic import OBJ_DICT, init_weights, make_batch  # noqa: E402
 
 METRIC = "crops/sec at 640×480 RGB-D, 1000 sampled pts; ADD(-S) AUC vs reference"
@@ -441,10 +441,10 @@ def main():
                          "LineMOD test-crop histogram, bucketed by S and every bucket split across the ranks "
                          "(distributed.bucket_shard; strong scaling: the 256 crops are shared by the N GPUs)")
     ap.add_argument("--global-batch", type=int, default=256, help="config 3: crops per step over all ranks")
-    ap.add_argument("--pipeline", choices=["none", "backbone", "heads", "pose"], default="heads",
-                    help="two-stage pipeline (pipeline.PipelinedPipeline) split after the backbone, the heads "
-                         "(default: 16.0-16.3 vs 16.3-16.5 ms/step) or before get_pose: stage A of batch k+1 runs "
-                         "beside stage B of batch k; none: one batch per step end to end")
+    ap.add_argument("--pipeline", choices=["none", "backbone", "heads", "pose"], default="none",
+                    help="none (default): one batch per step end to end as one hipGraph; backbone / heads / pose: "
+                         "the two-stage pipeline (pipeline.PipelinedPipeline) split there, whose stages overlap only "
+                         "with KRRN_STREAMS=1 (not reproducible on this stack, DESIGN.md §5; measured no faster)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -550,8 +550,9 @@ def main():
                        "graph": step is not None and step.graph is not None,
                        "micro_batches": args.micro,
                        "pipeline": "none" if isinstance(step, BatchPipeline) or step is None else
-                       f"2-stage split after the {args.pipeline} (stage A of batch k+1 beside stage B of batch k; "
-                       "one batch completes per step)"},
+                       f"2-stage split after the {args.pipeline} (stage A of batch k+1 "
+                       f"{'beside' if STREAMS else 'after'} stage B of batch k; one batch completes per step)",
+                       "graph_branches": PLAN_STREAMS},
             **extra,
             "roofline": roof, "cpu_baseline": cpu, "accuracy": acc,
         }

@@ -22,7 +22,7 @@ import torch
 
 from .krrn import KRRN, KRRNPlan
 from .pose import add_pose_ops
-from .runtime import Plan, ptr
+from .runtime import STREAMS, Plan, ptr
 
 
 @dataclass
@@ -121,7 +121,9 @@ class BatchPipeline:
         `concurrent` (used under hipGraph capture only, see runtime.Plan) the plans' side streams
         and the micro-batches' streams fork and join back."""
         serial = not concurrent
-        if not self.streams or serial:
+        if not self.streams or serial or not STREAMS:
+            # one part after the other on the caller's stream (under capture each part's plan keeps
+            # its graph branches; parts side by side on their streams only with KRRN_STREAMS=1)
             for pt in self.parts:
                 self._run_part(pt, serial)
             return
@@ -233,6 +235,11 @@ class PipelinedPipeline:
 
     def _half(self, run_a, run_b):
         b, a = self.h, self.h ^ 1
+        if not STREAMS:  # the two stages one after the other on the caller's stream (runtime.Plan)
+            run_b(b)
+            run_a(a)
+            self.h ^= 1
+            return
         main = torch.cuda.current_stream(self.device)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):

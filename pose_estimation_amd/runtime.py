@@ -134,6 +134,11 @@ class Sync:
 # A what-if timing diagnostic (profiles/whatif.sh: how much the step shrinks if a kernel family
 # were free); the outputs are meaningless with it set, and nothing in the package sets it.
 _DIAG_DROP = frozenset(filter(None, os.environ.get("KRRN_DIAG_DROP", "").split(",")))
+# KRRN_PLAN_STREAMS=1 (default): a plan captured into a hipGraph keeps its side streams (graph
+# branches); 0 = captured serially. KRRN_STREAMS=1: the two-slot pipeline's stages and concurrent
+# micro-batches replay side by side on two streams; default 0 = one after the other (Plan)
+PLAN_STREAMS = os.environ.get("KRRN_PLAN_STREAMS", "1") == "1"
+STREAMS = os.environ.get("KRRN_STREAMS", "0") == "1"
 
 
 class Plan:
@@ -144,11 +149,14 @@ class Plan:
     HRNet branches and head towers use this to run concurrently (one small conv cannot fill 256
     CUs; four of them side by side fill more).
 
-    `run()` is serial by default (everything on the caller's stream). The side streams are used
+    `run()` is serial by default (everything on the caller's stream); the side streams are used
     only with `run(serial=False)` under hipGraph capture, where every fork / join becomes a graph
-    edge: run eagerly, the plan's ~7 streams share the GPU_MAX_HW_QUEUES = 4 hardware queues, and
-    under that sharing a kernel intermittently read an input its producer on another stream had
-    not finished (profiles/race_bisect.py) -- the captured graphs never did."""
+    edge (KRRN_PLAN_STREAMS=0 makes captured plans serial too). Eagerly, the plan's ~7 streams share
+    the GPU_MAX_HW_QUEUES = 4 hardware queues and a kernel intermittently read an input its producer
+    on another stream had not finished (round 2). One captured plan graph at a time has matched the
+    serial run in every check; two graphs replayed on two streams at once (the
+    two-slot pipeline, concurrent micro-batches) did not, so those overlap only with KRRN_STREAMS=1
+    (pipeline.py)."""
 
     def __init__(self, device: torch.device):
         self.device = device
@@ -216,6 +224,7 @@ class Plan:
         return main
 
     def run(self, env: Dict[str, Any], serial: bool = True):
+        serial = serial or not PLAN_STREAMS
         self._streams(env, serial)
         for op in self.ops:
             op(env)

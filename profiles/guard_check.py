@@ -23,11 +23,12 @@ def guarded_buf(self, shape, dtype=torch.float32, zero=True):
     for s in shape:
         n *= int(s)
     es = torch.empty((), dtype=dtype).element_size()
-    raw = torch.empty(n * es + GUARD, dtype=torch.uint8, device=self.device)
+    # [guard | data | guard]: writes past either end land in a guard
+    raw = torch.empty(n * es + 2 * GUARD, dtype=torch.uint8, device=self.device)
+    raw.fill_(PAT)
     if zero:
-        raw[:n * es].zero_()
-    raw[n * es:].fill_(PAT)
-    t = raw[:n * es].view(dtype).view(tuple(shape))
+        raw[GUARD:GUARD + n * es].zero_()
+    t = raw[GUARD:GUARD + n * es].view(dtype).view(tuple(shape))
     self.buffers.append(raw)
     where = [f for f in traceback.extract_stack()[:-1] if "pose_estimation_amd" in f.filename][-2:]
     records.append((raw, n * es, tuple(shape), dtype, "; ".join(f"{os.path.basename(f.filename)}:{f.lineno}"
@@ -53,10 +54,10 @@ for _ in range(3):
 torch.cuda.synchronize()
 bad = 0
 for raw, nb, shape, dtype, where in records:
-    g = raw[nb:]
-    if not bool((g == PAT).all()):
-        idx = torch.nonzero(g != PAT).flatten()
-        bad += 1
-        print(f"OVERWRITTEN guard of {shape} {dtype} from {where}: {idx.numel()} bytes, first at +{int(idx[0])}, "
-              f"last at +{int(idx[-1])}", flush=True)
+    for side, g in (("after", raw[GUARD + nb:]), ("before", raw[:GUARD])):
+        if not bool((g == PAT).all()):
+            idx = torch.nonzero(g != PAT).flatten()
+            bad += 1
+            print(f"OVERWRITTEN guard {side} {shape} {dtype} from {where}: {idx.numel()} bytes, first at "
+                  f"+{int(idx[0])}, last at +{int(idx[-1])}", flush=True)
 print(f"B={B} S={S} N={N} {bb}: {len(records)} buffers checked, {bad} guards overwritten", flush=True)

@@ -62,9 +62,17 @@ with torch.cuda.stream(s):
     with torch.cuda.graph(gr, stream=s):
         plan.run(kp.env, serial=False)
 torch.cuda.current_stream().wait_stream(s)
-gr.replay()
-torch.cuda.synchronize()
-gra = snap()
+reps = int(os.environ.get("REPS", "1"))
+gra = None
+for r in range(reps):  # intermittent orderings: every replay must equal the serial run
+    gr.replay()
+    torch.cuda.synchronize()
+    cur = snap()
+    nbad = sum(not torch.equal(a, b) for a, b in zip(ser, cur))
+    if reps > 1:
+        print(f"replay {r}: {nbad} buffers differ", flush=True)
+    if gra is None or nbad:
+        gra = cur
 print(f"plan: {len(plan.ops)} ops, {len(bufs)} buffers, streams {plan.nstreams}", flush=True)
 for name, other in (("serial-again", ser2), ("eager-multistream", eag), ("graph", gra)):
     bad = [bi for bi in range(len(bufs)) if not torch.equal(ser[bi], other[bi])]

@@ -191,3 +191,32 @@ def test_pipelined_graph_benched_shape(dev):
         got = _snap(pp)
         for k in ref:
             assert torch.equal(got[k], ref[k]), (rep, k)
+
+
+def test_benched_step_graph_after_history(dev):
+    """bench.py's step as benched (config 2: one hipGraph of the whole path, every launch on one
+    stream, runtime.STREAMS off) after the allocation history above: graph replays alternating
+    between two RNG states each equal the eager serial step of that state bit for bit (a replay that
+    read a buffer before this step wrote it would see the other state's values)."""
+    _history(dev)
+    B, S, N = 64, 120, 1000
+    m = KRRN(cfg=make_config(num_cls=1, backbone="w18"))
+    init_weights(m, 0)
+    m = m.to(dev).eval()
+    pl = BatchPipeline(m, B, S, N, dev, parts=1, seed=0)
+    pl.load(make_batch(B, S, N, seed=1))
+    seeds = [pl.parts[0].kp.seed.clone(), pl.parts[0].kp.seed.clone() + 12345]
+    refs = []
+    for sd in seeds:
+        pl.parts[0].kp.seed.copy_(sd)
+        pl.run()
+        torch.cuda.synchronize()
+        refs.append(_snap(pl))
+    pl.capture()
+    for rep in range(4):
+        pl.parts[0].kp.seed.copy_(seeds[rep % 2])
+        pl.step()
+        torch.cuda.synchronize()
+        got = _snap(pl)
+        for k in refs[rep % 2]:
+            assert torch.equal(got[k], refs[rep % 2][k]), (rep, k)
