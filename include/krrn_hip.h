@@ -140,6 +140,15 @@ int krrn_gemm_x3_gather_f32(const int* ia, const float* A, long long a_bs, int a
                             long long a2_bs, int a2_st, int npts, int B, int K, int N, const void* w3f,
                             const float* bias, float* out, int ldo, int relu, void* stream);
 
+/* krrn_conv_small_f32 on the bf16 matrix cores at f32 accuracy (conv_small.hip, X3 form): the
+ * staged input split into three exact bf16 terms, six term products per f32 product on
+ * v_mfma_f32_16x16x32_bf16 (2.67x the f32 MFMA rate). w3: ops.quad_weights_x3 planes of the same
+ * [N][taps * cin] weights; every other argument and check as krrn_conv_small_f32. */
+int krrn_conv_small_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* w3,
+                           int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
+                           int res_co, float* out, int out_cs, int out_co, int relu, int ksize, int stride, int nw,
+                           int ks, void* stream);
+
 /* One HRNet BasicBlock without downsample (conv_bb.hip; lib/network/hrnet/myhrnet.py:34-63):
  *   out = ReLU(s2 * conv3x3(ReLU(s1 * conv3x3(in) + b1)) + b2 + in)
  * on NHWC rows (channel stride / offset in_cs / in_co, out_cs / out_co; C padded channels, a

@@ -53,6 +53,11 @@ CONV_X3 = os.environ.get("KRRN_CONV_X3", "1") == "1"
 # per block (0 = ops.bb_tile_rows). Off by default: measured slower in the step (DESIGN.md §3,
 # "Fused BasicBlock"): 12.81 vs 12.42 ms with the 20 / 36-channel branches fused, 13.43 with all
 BB_FUSED = os.environ.get("KRRN_BB", "0") == "1"
+# the small direct convs on split-bf16 operands (krrn_conv_small_x3_f32) instead of f32 MFMAs: off by
+# default, measured slower (profiles/bench_small.py X3=1: 24.4 / 14.1 / 14.1 / 16.2 vs 18.9 / 13.3 /
+# 13.2 / 14.2 us; step 5000 vs 5202 crops/s): the latency-bound K loop gains nothing from the faster
+# MFMAs and pays for the split staging, the doubled LDS slab and 1.5x the weight bytes
+SMALL_X3 = os.environ.get("KRRN_SMALL_X3", "0") == "1"
 BB_T = int(os.environ.get("KRRN_BB_T", "0"))
 # widest block (16-channel tiles) taken: the 72 / 144-channel branches measured no faster fused than
 # as two conv_small launches (profiles/bench_bb.py: their long K chains leave little MFMA work per
@@ -279,7 +284,13 @@ class _Builder:
 
     def emit_small(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         p = self.small_problem(x, spec, out, res, relu)
-        self.plan.add("krrn_conv_small_f32", p["x"], p["in_cs"], p["in_co"], p["B"], p["H"], p["W"], p["cin"], p["wt"],
+        name = "krrn_conv_small_f32"
+        if SMALL_X3:  # split-bf16 operands on the bf16 matrix cores (f32 accuracy)
+            w3 = ops.quad_weights_x3(spec.wt[0], p["N"], spec.ksize ** 2 * spec.cin_p)
+            self.specs.append(w3)
+            p["wt"] = ptr(w3)
+            name = "krrn_conv_small_x3_f32"
+        self.plan.add(name, p["x"], p["in_cs"], p["in_co"], p["B"], p["H"], p["W"], p["cin"], p["wt"],
                       p["N"], p["n_store"], p["scale"], p["bias"], p["res"], p["res_cs"], p["res_co"], p["out"],
                       p["out_cs"], p["out_co"], p["relu"], p["ksize"], p["stride"], p["nw"], p["ks"],
                       meta=dict(kernel=f"conv_small<{p['nw']},{p['ks']}>", flops=p["flops"], tag=tag, M=p["M"], N=p["N"],

@@ -286,22 +286,28 @@ def gemm_weights_x3(wt: torch.Tensor) -> torch.Tensor:
     return c.permute(0, 2, 4, 3, 1, 5).contiguous()                 # nb g q fh nl 4
 
 
-def bb_weights_x3(wt: torch.Tensor, C: int) -> torch.Tensor:
-    """A BasicBlock conv's weights [N >= C][9 C] f32 (k = tap * C + c, ops.make_conv's packing) ->
-    the split planes krrn_basic_block_x3_f32 reads, int32: the [m h] plane [NTt*16][KQp][4]
-    (per output channel and channel quad kq: m0..m3 h0..h3 bf16) then the [l] plane [NTt*16][KQp][2]
-    (l0..l3); NTt = ceil(C / 16) channel tiles, KQp = 9 C / 4 rounded up to a multiple of 16 (the
-    kernel runs its reduction in groups of 4 steps of 4 quads), zero padded (padding channels /
-    quads contribute exact zeros)."""
-    ntt = (C + 15) // 16
-    kqp = -(-(9 * C // 4) // 16) * 16
-    w = torch.zeros(ntt * 16, kqp * 4, dtype=torch.float32, device=wt.device)
-    n = min(wt.shape[0], C)
-    w[:n, :9 * C] = wt.reshape(wt.shape[0], -1)[:n, :9 * C].float()
-    h, m, l = (t.reshape(ntt * 16, kqp, 4) for t in split_bf16x3(w))
+def quad_weights_x3(wt: torch.Tensor, N: int, K: int, kq_mult: int = 4) -> torch.Tensor:
+    """Conv weights [>= N][>= K] f32 (k = tap * cin + c, ops.make_conv's packing) -> the split planes
+    the channel-quad kernels read (krrn_conv_small_x3_f32, krrn_basic_block_x3_f32), int32: the
+    [m h] plane [N16][KQp][4] (per output channel and channel quad kq: m0..m3 h0..h3 bf16) then the
+    [l] plane [N16][KQp][2] (l0..l3); N16 = N rounded up to 16, KQp = K / 4 rounded up to a
+    multiple of kq_mult, zero padded (padding channels / quads contribute exact zeros)."""
+    n16 = (N + 15) // 16 * 16
+    kqp = -(-(K // 4) // kq_mult) * kq_mult
+    w = torch.zeros(n16, kqp * 4, dtype=torch.float32, device=wt.device)
+    n = min(wt.shape[0], N)
+    w[:n, :K] = wt.reshape(wt.shape[0], -1)[:n, :K].float()
+    h, m, l = (t.reshape(n16, kqp, 4) for t in split_bf16x3(w))
     mh = torch.cat([m, h], dim=-1).contiguous().view(torch.int32).reshape(-1)
     lp = l.contiguous().view(torch.int32).reshape(-1)
     return torch.cat([mh, lp]).contiguous()
+
+
+def bb_weights_x3(wt: torch.Tensor, C: int) -> torch.Tensor:
+    """A BasicBlock conv's weights [N >= C][9 C] -> krrn_basic_block_x3_f32's planes
+    (quad_weights_x3 with the quads padded to a multiple of 16: the kernel runs its reduction in
+    groups of 4 steps of 4 quads)."""
+    return quad_weights_x3(wt, C, 9 * C, kq_mult=16)
 
 
 def bb_tile_rows(B: int, H: int, W: int, C: int, max_lds: int = 160 * 1024) -> int:

@@ -57,6 +57,7 @@ _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])
 _lib.register("krrn_gemm_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, L, L, L, P])
+_lib.register("krrn_conv_small_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, I, I, I, I, P])
 _lib.register("krrn_basic_block_x3_f32", [P, I, I, I, I, I, I, P, P, P, P, P, P, P, I, I, I, P])
 _lib.register("krrn_gemm_x3_gather_f32", [P, P, L, I, P, P, L, I, I, I, I, I, P, P, P, I, I, P])
 _lib.register("krrn_gemm_panel_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, P])

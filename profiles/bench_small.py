@@ -20,7 +20,7 @@ B = int(os.environ.get("B", 64))
 shapes = [(20, 30), (36, 15), (72, 8), (144, 4)]  # (padded C, side)
 L = _lib.lib()
 st = P(torch.cuda.current_stream().cuda_stream)
-tag = os.path.basename(os.environ.get("KRRN_HIP_LIB", "in-tree"))
+tag = os.path.basename(os.environ.get("KRRN_HIP_LIB", "in-tree")) + (" x3" if os.environ.get("X3") == "1" else "")
 for cp, H in shapes:
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, H, H, cp, generator=g).to(dev)
@@ -31,9 +31,12 @@ for cp, H in shapes:
     out = torch.zeros(B, H, H, cp, device=dev)
     nw, ks = ops.small_conv_config(B * H * H, (cp + 15) // 16, cp)
 
+    w3 = ops.quad_weights_x3(w, cp, 9 * cp)
+    fn, wp = (L.krrn_conv_small_x3_f32, w3) if os.environ.get("X3") == "1" else (L.krrn_conv_small_f32, w)
+
     def run():
-        _lib.check(L.krrn_conv_small_f32(ptr(x), cp, 0, B, H, H, cp, ptr(w), cp, cp, ptr(sc), ptr(bi), ptr(res), cp, 0,
-                                         ptr(out), cp, 0, 1, 3, 1, nw, ks, st), "small")
+        _lib.check(fn(ptr(x), cp, 0, B, H, H, cp, ptr(wp), cp, cp, ptr(sc), ptr(bi), ptr(res), cp, 0,
+                      ptr(out), cp, 0, 1, 3, 1, nw, ks, st), "small")
     run()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -388,3 +388,42 @@ def test_conv1x1_nchw(dev, B, HW, cin, cout, co, oc, Cx):
     torch.testing.assert_close(out[:, oc:oc + cout].cpu(), ref, **TOL)
     if oc:
         assert torch.isnan(out[:, :oc]).all()
+
+
+@pytest.mark.parametrize("B,cin,cout,H,k,st,nw,ks", [
+    (3, 18, 18, 30, 3, 1, 2, 1), (3, 36, 36, 15, 3, 1, 3, 2), (4, 72, 72, 8, 3, 1, 3, 4), (4, 144, 144, 4, 3, 1, 3, 4),
+    (3, 36, 72, 15, 3, 2, 3, 4), (4, 72, 20, 8, 1, 1, 2, 4)])
+def test_conv_small_x3(dev, B, cin, cout, H, k, st, nw, ks):
+    """krrn_conv_small_x3_f32 (split-bf16 operands) vs torch: f32 tolerance, f32-level error against
+    an f64 evaluation, residual + ReLU, pad channels zero."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, ptr
+    g = torch.Generator().manual_seed(cin * cout + H + 7 * k + st + 1)
+    conv = nn.Conv2d(cin, cout, k, st, (k - 1) // 2, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / (k * cin ** 0.5))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, H, generator=g)
+    with torch.no_grad():
+        y = bn(conv(x))
+        y64 = bn.double()(conv.double()(x.double()))
+    Ho = y.shape[2]
+    res = torch.randn(B, cout, Ho, Ho, generator=g)
+    ref, ref64 = torch.relu(y + res), torch.relu(y64 + res.double())
+    xa = _nhwc(x, dev)
+    spec = ops.make_conv(conv.float(), bn.float(), dev, cin_p=ops.pad4(cin))
+    np_ = ops.pad4(cout)
+    w3 = ops.quad_weights_x3(spec.wt[0], np_, k * k * ops.pad4(cin))
+    ra = _nhwc(res, dev)
+    out = torch.full((B, Ho, Ho, np_), float("nan"), device=dev)
+    _lib.check(_lib.lib().krrn_conv_small_x3_f32(ptr(xa.t), xa.cs, 0, B, H, H, ops.pad4(cin), ptr(w3), np_, np_,
+                                                 ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out), np_,
+                                                 0, 1, k, st, nw, ks, P(torch.cuda.current_stream().cuda_stream)),
+               "small conv x3")
+    torch.cuda.synchronize()
+    got = out[..., :cout].permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, **TOL)
+    err = float((got.double() - ref64).abs().max())
+    err32 = float((ref.double() - ref64).abs().max())
+    assert err <= max(4 * err32, 2e-6 * float(ref64.abs().max())), (err, err32)
+    assert torch.count_nonzero(out[..., cout:np_]).item() == 0
