@@ -179,6 +179,12 @@ int krrn_conv1x1_nchw_f32(const float* in, int in_cs, int in_co, int B, int HW, 
                           int n_store, const float* scale, const float* bias, float* out, int out_cs, int out_co,
                           void* stream);
 
+/* krrn_conv1x1_nchw_f32 on split-bf16 operands (f32 accuracy; the same output): cin = 128 and w3
+ * the split weight planes of ops.quad_weights_x3(wt, N, 128) (16-byte aligned). */
+int krrn_conv1x1_nchw_x3_f32(const float* in, int in_cs, int in_co, int B, int HW, int cin, const void* w3, int N,
+                             int n_store, const float* scale, const float* bias, float* out, int out_cs, int out_co,
+                             void* stream);
+
 /* 3x3 stride-1 pad-1 convolution by fused Winograd F(2x2, 3x3) (the head / last_layer /
  * deconv-BasicBlock convs: krrn.py:46-84, myhrnet.py:324-346; cuDNN / MIOpen use the same
  * algorithm for these f32 convs). U = G g G^T are the transformed weights, f32 in chunk-major

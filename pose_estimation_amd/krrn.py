@@ -44,6 +44,10 @@ from .ops import Act, pad4
 from .posenet import PoseNet, build_tbase_plan, emit_tbase_level1
 from .runtime import Late, Plan, add_conv, ptr
 
+# the wide head's final 1x1 conv (xyz_final, K = 128) on split-bf16 operands (f32 accuracy,
+# krrn_conv1x1_nchw_x3_f32) instead of f32 MFMAs
+NCHW_X3 = os.environ.get("KRRN_NCHW_X3", "1") == "1"
+
 
 TBASE_EARLY = os.environ.get("KRRN_TBASE_EARLY", "1") == "1"
 # KRRN.forward replays a hipGraph of its plan (captured after one serial warm-up run): the only
@@ -208,7 +212,11 @@ class KRRNPlan:
         B, Cx, Ho, Wo = out.shape
         np_ = pad4(spec.cout)
         if len(spec.taps[0]) == 1 and spec.stride == 1 and spec.cin_p <= 256 and np_ <= 80:
-            self.plan.add("krrn_conv1x1_nchw_f32", ptr(x.t), x.cs, x.co, x.B, Ho * Wo, spec.cin_p, ptr(spec.wt[0]), np_,
+            name, wt = "krrn_conv1x1_nchw_f32", spec.wt[0]
+            if NCHW_X3 and spec.cin_p == 128 and np_ > 48:  # split-bf16 MFMAs, weights held in registers
+                name, wt = "krrn_conv1x1_nchw_x3_f32", ops.quad_weights_x3(spec.wt[0], np_, 128)
+                self.plan.buffers.append(wt)
+            self.plan.add(name, ptr(x.t), x.cs, x.co, x.B, Ho * Wo, spec.cin_p, ptr(wt), np_,
                           n_store, ptr(spec.scale), ptr(spec.bias), ptr(out), Cx, 0,
                           meta=dict(kernel="conv1x1_nchw", flops=2.0 * spec.cin * n_store * B * Ho * Wo,
                                     tag="head_final", M=B * Ho * Wo, N=np_, K=spec.cin_p, splits=1,

@@ -51,6 +51,7 @@ _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I
 _lib.register("krrn_wino_variant", [I])
 _lib.register("krrn_conv3x3_wino_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv1x1_nchw_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
+_lib.register("krrn_conv1x1_nchw_x3_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
 _lib.register("krrn_conv_small_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, I, I, I, I, P])
 _lib.register("krrn_conv_small_group_f32", [P, I, P])
 _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L, P, P])

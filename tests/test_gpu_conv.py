@@ -390,6 +390,43 @@ def test_conv1x1_nchw(dev, B, HW, cin, cout, co, oc, Cx):
         assert torch.isnan(out[:, :oc]).all()
 
 
+@pytest.mark.parametrize("B,HW,cout,co,oc,Cx", [(3, 1000, 72, 0, 0, 72), (2, 777, 72, 4, 0, 72), (4, 64, 20, 0, 5, 30),
+                                                (1, 130, 80, 0, 0, 80), (2, 1000, 50, 8, 3, 60), (2, 4, 72, 0, 0, 72),
+                                                (5, 4800, 72, 0, 0, 72)])
+def test_conv1x1_nchw_x3(dev, B, HW, cout, co, oc, Cx):
+    """krrn_conv1x1_nchw_x3_f32 (split-bf16 operands, the xyz head's final conv) vs torch fp32 and an
+    f64 evaluation: ragged pixel tiles, odd HW (the scalar NCHW store), channel-offset input and
+    output, nothing written outside the output slice."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, ptr
+    cin = 128
+    g = torch.Generator().manual_seed(HW + cout + 3)
+    W = HW // 2 if HW % 2 == 0 else HW
+    H = HW // W
+    conv = nn.Conv2d(cin, cout, 1, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
+        conv.bias.copy_(torch.randn(cout, generator=g))
+    x = torch.randn(B, cin, H, W, generator=g)
+    with torch.no_grad():
+        ref = conv(x)
+        ref64 = conv.double()(x.double())
+    xa = _nhwc(x, dev, cs=cin + co + 4, co=co)
+    spec = ops.make_conv(conv.float(), None, dev, cin_p=cin)
+    w3 = ops.quad_weights_x3(spec.wt[0], ops.pad4(cout), cin)
+    out = torch.full((B, Cx, H, W), float("nan"), device=dev)
+    _lib.check(_lib.lib().krrn_conv1x1_nchw_x3_f32(ptr(xa.t), xa.cs, xa.co, B, HW, cin, ptr(w3), ops.pad4(cout), cout,
+                                                   ptr(spec.scale), ptr(spec.bias), ptr(out), Cx, oc,
+                                                   P(torch.cuda.current_stream().cuda_stream)), "conv1x1 nchw x3")
+    torch.cuda.synchronize()
+    got = out[:, oc:oc + cout].cpu()
+    torch.testing.assert_close(got, ref, **TOL)
+    err = float((got.double() - ref64).abs().max())
+    err32 = float((ref.double() - ref64).abs().max())
+    assert err <= max(4 * err32, 2e-6 * float(ref64.abs().max())), (err, err32)
+    assert torch.isnan(out[:, :oc]).all() and torch.isnan(out[:, oc + cout:]).all()
+
+
 @pytest.mark.parametrize("B,cin,cout,H,k,st,nw,ks", [
     (3, 18, 18, 30, 3, 1, 2, 1), (3, 36, 36, 15, 3, 1, 3, 2), (4, 72, 72, 8, 3, 1, 3, 4), (4, 144, 144, 4, 3, 1, 3, 4),
     (3, 36, 72, 15, 3, 2, 3, 4), (4, 72, 20, 8, 1, 1, 2, 4)])
