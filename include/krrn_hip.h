@@ -180,7 +180,7 @@ int krrn_conv1x1_nchw_f32(const float* in, int in_cs, int in_co, int B, int HW, 
                           void* stream);
 
 /* krrn_conv1x1_nchw_f32 on split-bf16 operands (f32 accuracy; the same output): cin = 128 and w3
- * the split weight planes of ops.quad_weights_x3(wt, N, 128) (16-byte aligned). */
+ * the split weight planes of ops.quad_weights_x3(wt, N, 128) (16-byte aligned); 32 < N <= 80. */
 int krrn_conv1x1_nchw_x3_f32(const float* in, int in_cs, int in_co, int B, int HW, int cin, const void* w3, int N,
                              int n_store, const float* scale, const float* bias, float* out, int out_cs, int out_co,
                              void* stream);

@@ -123,13 +123,15 @@ __global__ __launch_bounds__(256) void conv1x1_nchw_kernel(const float* __restri
   }
 }
 
-// Split-bf16 form (X3) for the wide head (xyz_final: K = 128, N = 72 -> 5 channel tiles): block =
-// NT waves, wave w owns channel tile w for the whole K with its [m h l] weight chains in registers
-// for the block's life (8 steps x 6 VGPRs, loaded once), so LDS holds only the staged pixel rows,
-// split into [h h] / [m l] planes (67.6 KB: two blocks per CU). Per 16 k and 16-pixel subtile three
+// Split-bf16 form (X3) for the wide head (xyz_final: K = 128, N = 72 -> 5 channel tiles). The
+// block-staged form above is latency-bound on its input (one 32-KB tile in flight per block between
+// barriers: ~2.6 TB/s); here every wave streams its own 16-pixel subtiles with no block barrier
+// after the weight fill: the block's LDS holds all NT channel tiles' split weights in lane order
+// ([tile][step][64 lanes], conflict-free 16 / 8-B reads), a lane loads its pixel's channel quad of
+// each step straight from HBM (next subtile's 8 quads prefetched into registers) and splits it
+// in registers into [h h] / [m l] operands. Per 16 k and channel tile three
 // v_mfma_f32_16x16x32_bf16 (W[h l] x X[h h], W[m h] x X[h m], W[m h] x X[m l]: the six term
-// products hh lh mh hm mm hl at f32 accuracy, 2.67x the f32 MFMA rate). Same output layout and
-// NCHW store path as the f32 kernel.
+// products hh lh mh hm mm hl at f32 accuracy).
 typedef __bf16 nx_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 nx_bf16x2 __attribute__((ext_vector_type(2)));
 typedef float nx_f32x2 __attribute__((ext_vector_type(2)));
@@ -151,114 +153,180 @@ __device__ __forceinline__ void nx_split(const f32x4 x, nx_u32x4& p0, nx_u32x4& 
 }
 __device__ __forceinline__ nx_bf16x8 nx_op(const nx_u32x4 v) { return __builtin_bit_cast(nx_bf16x8, v); }
 
-constexpr int kX3Steps = 8;          // K = 128: 8 steps of 16 k (4 channel quads x 4 lane groups)
-constexpr int kX3Q = 4 * kX3Steps;   // channel quads per pixel
-constexpr int kX3Pitch = kX3Q + 1;   // 16-B slots per staged pixel and plane (odd: conflict-free)
+constexpr int kX3Steps = 8;         // K = 128: 8 steps of 16 k (4 channel quads x 4 lane groups)
+constexpr int kX3Q = 4 * kX3Steps;  // channel quads per pixel
+constexpr int kX3Waves = 8;
 
 template <int NT>
-__global__ __launch_bounds__(64 * NT) void conv1x1_nchw_x3_kernel(const float* __restrict__ in, int in_cs, int in_co,
-                                                                  int B, int HW, const unsigned* __restrict__ w3,
-                                                                  int n_store, const float* __restrict__ scale,
-                                                                  const float* __restrict__ bias, float* __restrict__ out,
-                                                                  int out_cs, int out_co, int vec) {
-  constexpr int kThreads = 64 * NT;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  nx_u32x4* sx0 = reinterpret_cast<nx_u32x4*>(lds);  // [kPx][kX3Pitch] planes [h h], then [m l]
-  nx_u32x4* sx1 = sx0 + kPx * kX3Pitch;
+__global__ __launch_bounds__(64 * kX3Waves) __attribute__((amdgpu_waves_per_eu(4))) void conv1x1_nchw_x3_kernel(const float* __restrict__ in, int in_cs,
+                                                                        int in_co, int B, int HW,
+                                                                        const unsigned* __restrict__ w3, int n_store,
+                                                                        const float* __restrict__ scale,
+                                                                        const float* __restrict__ bias,
+                                                                        float* __restrict__ out, int out_cs,
+                                                                        int out_co) {
+  __shared__ nx_u32x4 smh[NT * kX3Steps * 64];  // [tile][step][lane]: m0..m3 h0..h3
+  __shared__ nx_u32x2 sl[NT * kX3Steps * 64];   // l0..l3
+  __shared__ float ssc[16 * NT], sbi[16 * NT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  const int tpi = krrn_cdiv(HW, kPx), ntiles = B * tpi;
-  // this wave's weight chains for the whole K (record = channel x quad; quads of step st: 4 st + g)
-  const unsigned nrec = (unsigned)(16 * NT * kX3Q);
-  const nx_u32x4* wmh_g = reinterpret_cast<const nx_u32x4*>(w3);
-  const nx_u32x2* wl_g = reinterpret_cast<const nx_u32x2*>(w3 + 4 * nrec);
-  nx_u32x4 wmh[kX3Steps];
-  nx_u32x2 wl[kX3Steps];
-#pragma unroll
-  for (int st = 0; st < kX3Steps; ++st) {
-    const int r = (16 * wave + fr) * kX3Q + 4 * st + g;
-    wmh[st] = wmh_g[r];
-    wl[st] = wl_g[r];
+  {
+    const unsigned nrec = (unsigned)(16 * NT * kX3Q);
+    const nx_u32x4* wmh_g = reinterpret_cast<const nx_u32x4*>(w3);
+    const nx_u32x2* wl_g = reinterpret_cast<const nx_u32x2*>(w3 + 4 * nrec);
+    for (int e = tid; e < NT * kX3Steps * 64; e += 64 * kX3Waves) {
+      const int l = e & 63, ts = e >> 6, t = ts / kX3Steps, st = ts - t * kX3Steps;
+      const int r = (16 * t + (l & 15)) * kX3Q + 4 * st + (l >> 4);
+      smh[e] = wmh_g[r];
+      sl[e] = wl_g[r];
+    }
+    for (int n = tid; n < 16 * NT; n += 64 * kX3Waves) {
+      ssc[n] = n < n_store && scale ? scale[n] : 1.f;
+      sbi[n] = n < n_store && bias ? bias[n] : 0.f;
+    }
   }
-  constexpr int kItems = kPx * kX3Q;  // float4 per tile
-  constexpr int kU = (kItems + kThreads - 1) / kThreads;
-  auto load_x = [&](int tile, f32x4 (&r)[kU]) {
-    const int b = tile / tpi, px0 = (tile - b * tpi) * kPx;
-    const float* xb = in + ((long long)b * HW) * in_cs + in_co;
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = tid + kThreads * u;
-      const int p = e / kX3Q, q = e - (e / kX3Q) * kX3Q;
-      r[u] = (e < kItems && px0 + p < HW) ? *reinterpret_cast<const f32x4*>(xb + (long long)(px0 + p) * in_cs + 4 * q)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+  __syncthreads();
+  const int spi = krrn_cdiv(HW, 16), nsub = B * spi;
+  auto x_ptr = [&](int c, bool& ok) {
+    const int b = c / spi, px = (c - b * spi) * 16 + fr;
+    ok = px < HW;
+    return in + ((long long)b * HW + px) * in_cs + in_co + 4 * g;
   };
-  f32x4 xn[kU];
-  if (blockIdx.x < ntiles) load_x(blockIdx.x, xn);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    __syncthreads();  // the previous tile's MFMAs / output transpose are done with the planes
+  const int stride = gridDim.x * kX3Waves;
+  int c = blockIdx.x * kX3Waves + wave;
+  // xr[st]: this subtile's quad of step st; once split, the register takes the next subtile's quad
+  // (in flight for a whole subtile of MFMAs)
+  f32x4 xr[kX3Steps];
+  if (c < nsub) {
+    bool ok;
+    const float* xp = x_ptr(c, ok);
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int e = tid + kThreads * u;
-      if (e < kItems) {
-        const int p = e / kX3Q, q = e - (e / kX3Q) * kX3Q;
-        nx_u32x4 p0, p1;
-        nx_split(xn[u], p0, p1);
-        sx0[p * kX3Pitch + q] = p0;
-        sx1[p * kX3Pitch + q] = p1;
-      }
-    }
-    __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) load_x(tile + gridDim.x, xn);  // in flight under the MFMAs
-    f32x4 acc[4];
+    for (int st = 0; st < kX3Steps; ++st)
+      xr[st] = ok ? *reinterpret_cast<const f32x4*>(xp + 16 * st) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (; c < nsub; c += stride) {
+    const bool more = c + stride < nsub;
+    bool nok = false;
+    const float* np = more ? x_ptr(c + stride, nok) : in;
+    nok = nok && more;
+    f32x4 acc[NT];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int wl_off = lane;  // made opaque per step: keeps the weight reads in the loop, one step live at a time
 #pragma unroll
     for (int st = 0; st < kX3Steps; ++st) {
-      const nx_u32x4 whl = nx_u32x4{wmh[st][2], wmh[st][3], wl[st][0], wl[st][1]};
+      asm volatile("" : "+v"(wl_off));
+      nx_u32x4 x0, x1;
+      nx_split(xr[st], x0, x1);
+      if (more) xr[st] = nok ? *reinterpret_cast<const f32x4*>(np + 16 * st) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const nx_u32x4 xhm = nx_u32x4{x0[0], x0[1], x1[0], x1[1]};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int e = (16 * s + fr) * kX3Pitch + 4 * st + g;
-        const nx_u32x4 x0 = sx0[e], x1 = sx1[e];
-        const nx_u32x4 xhm = nx_u32x4{x0[0], x0[1], x1[0], x1[1]};
-        acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nx_op(whl), nx_op(x0), acc[s], 0, 0, 0);
-        acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nx_op(wmh[st]), nx_op(xhm), acc[s], 0, 0, 0);
-        acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nx_op(wmh[st]), nx_op(x1), acc[s], 0, 0, 0);
+      for (int t = 0; t < NT; ++t) {
+        const nx_u32x4 wmh = smh[(t * kX3Steps + st) * 64 + wl_off];
+        const nx_u32x2 wl = sl[(t * kX3Steps + st) * 64 + wl_off];
+        const nx_u32x4 whl = nx_u32x4{wmh[2], wmh[3], wl[0], wl[1]};
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nx_op(whl), nx_op(x0), acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nx_op(wmh), nx_op(xhm), acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nx_op(wmh), nx_op(x1), acc[t], 0, 0, 0);
       }
     }
-    // acc[s][i] = (channel 16 wave + 4 g + i, pixel 16 s + fr)
-    const int b = tile / tpi, px0 = (tile - b * tpi) * kPx;
-    if (vec) {
-      __syncthreads();
-      float* so = lds;  // [16 NT][kOP], over the planes (every wave's MFMAs are done)
+    // acc[t][i] = (channel 16 t + 4 g + i, pixel 16 (c % spi) + fr): 64-B NCHW runs per channel
+    const int b = c / spi, px = (c - b * spi) * 16 + fr;
+    if (px < HW) {
+      float* ob = out + ((long long)b * out_cs + out_co) * HW + px;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) so[(16 * wave + 4 * g + i) * kOP + 16 * s + fr] = acc[s][i];
-      __syncthreads();
-      float* ob = out + ((long long)b * out_cs + out_co) * HW + px0;
-      for (int e = tid; e < n_store * (kPx / 4); e += kThreads) {
-        const int n = e / (kPx / 4), q = e - n * (kPx / 4);
-        if (px0 + 4 * q >= HW) continue;  // HW % 4 == 0: a float4 is all in or all out
-        const float sc = scale ? scale[n] : 1.f, bi = bias ? bias[n] : 0.f;
-        f32x4 v = *reinterpret_cast<const f32x4*>(so + n * kOP + 4 * q);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] * sc + bi;
-        *reinterpret_cast<f32x4*>(ob + (long long)n * HW + 4 * q) = v;
-      }
-      continue;
+        for (int i = 0; i < 4; ++i) {
+          const int n = 16 * t + 4 * g + i;
+          if (n < n_store) ob[(long long)n * HW] = acc[t][i] * ssc[n] + sbi[n];
+        }
     }
+  }
+}
+
+// Narrow form (N <= 4 weight rows: the normal head's 3-channel conv, krrn.py:80-84): a pure HBM
+// read of the 128-channel rows, so no MFMA tile (16 of 16 rows would idle) and no LDS staging:
+// 8 lanes per pixel each read KQL channel quads (one 128-B run per 8 lanes and load), dot them
+// against their quads of the <= 4 weight rows held in registers, and an xor butterfly sums the 8
+// partials; each wave walks 32-pixel chunks (4 rounds of 8 pixels, all loads issued up front) and
+// writes them through a per-wave LDS row as 128-B NCHW runs.
+constexpr int kNarrowPx = 32;
+constexpr int kNarrowPitch = kNarrowPx + 4;
+
+template <int KQL>
+__global__ __launch_bounds__(256) void conv1x1_nchw_narrow_kernel(const float* __restrict__ in, int in_cs, int in_co,
+                                                                  int B, int HW, const float* __restrict__ wt, int N,
+                                                                  int n_store, const float* __restrict__ scale,
+                                                                  const float* __restrict__ bias,
+                                                                  float* __restrict__ out, int out_cs, int out_co,
+                                                                  int vec) {
+  constexpr int cin = 32 * KQL;
+  __shared__ __attribute__((aligned(16))) float so_all[4][4 * kNarrowPitch];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 7, k = lane >> 3;
+  float* so = so_all[wave];
+  f32x4 w[4][KQL];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int t = 0; t < KQL; ++t)
+      w[n][t] = n < N ? *reinterpret_cast<const f32x4*>(wt + n * cin + 4 * (j + 8 * t)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const int cpi = krrn_cdiv(HW, kNarrowPx), nch = B * cpi;
+  for (int c = blockIdx.x * 4 + wave; c < nch; c += gridDim.x * 4) {
+    const int b = c / cpi, px0 = (c - b * cpi) * kNarrowPx;
+    f32x4 x[4][KQL];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int p = px0 + 8 * it + k;
+      const float* xp = in + ((long long)b * HW + p) * in_cs + in_co + 4 * j;
+#pragma unroll
+      for (int t = 0; t < KQL; ++t)
+        x[it][t] = p < HW ? *reinterpret_cast<const f32x4*>(xp + 32 * t) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float acc[4][4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        float a = 0.f;
+#pragma unroll
+        for (int t = 0; t < KQL; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a = fmaf(x[it][t][i], w[n][t][i], a);
+        acc[it][n] = a;
+      }
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1)
+#pragma unroll
+      for (int it = 0; it < 4; ++it)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[it][n] += __shfl_xor(acc[it][n], off);
+    // every lane of pixel group k holds its 16 sums: lane j writes channel j & 3 of rounds 2 (j >> 2) + {0, 1}
+    {
+      const int n = j & 3;
+      const float sc = n < n_store && scale ? scale[n] : 1.f, bi = n < n_store && bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int it = 2 * (j >> 2) + r;
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int nn = 0; nn < 4; ++nn) v = (q == it && nn == n) ? acc[q][nn] : v;
+        so[n * kNarrowPitch + 8 * it + k] = v * sc + bi;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
     float* ob = out + ((long long)b * out_cs + out_co) * HW + px0;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int px = 16 * s + fr;
-      if (px0 + px >= HW) continue;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = 16 * wave + 4 * g + i;
-        if (n < n_store) ob[(long long)n * HW + px] = acc[s][i] * (scale ? scale[n] : 1.f) + (bias ? bias[n] : 0.f);
-      }
+    if (vec) {
+      const int n = lane >> 3, q = lane & 7;  // lanes 0..31: 4 channels x 8 float4
+      if (n < n_store && px0 + 4 * q < HW)
+        *reinterpret_cast<f32x4*>(ob + (long long)n * HW + 4 * q) = *reinterpret_cast<const f32x4*>(so + n * kNarrowPitch + 4 * q);
+    } else if (lane < kNarrowPx && px0 + lane < HW) {
+      for (int n = 0; n < n_store; ++n) ob[(long long)n * HW + lane] = so[n * kNarrowPitch + lane];
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -268,28 +336,24 @@ KRRN_API int krrn_conv1x1_nchw_x3_f32(const float* in, int in_cs, int in_co, int
                                       int N, int n_store, const float* scale, const float* bias, float* out, int out_cs,
                                       int out_co, void* stream) {
   if (!in || !w3 || !out) return KRRN_EARG;
-  if (B < 1 || HW < 1 || N < 1 || N > 80 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
+  // 3..5 channel tiles: the staged pixel rows fit the registers of 3+ waves (two blocks per CU)
+  if (B < 1 || HW < 1 || N <= 32 || N > 80 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
   if (cin != 4 * kX3Q) return KRRN_ESHAPE;  // the heads' 128-channel input (weights in registers)
   if ((in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
   if (!krrn_aligned16(in) || !krrn_aligned16(w3)) return KRRN_EALIGN;
   if (out_co + n_store > out_cs || (long long)B * HW * in_cs >= (1LL << 40)) return KRRN_ESHAPE;
   if ((long long)B * krrn_cdiv(HW, kPx) > 0x7fffffffLL) return KRRN_ESHAPE;
   const int nt = (N + 15) / 16;
-  const size_t lds = 2 * sizeof(nx_u32x4) * (size_t)kPx * kX3Pitch;  // >= the output tile 16 nt x kOP floats
-  const int ntiles = B * krrn_cdiv(HW, kPx);
-  const dim3 grid(min(ntiles, 256 * 2));
+  const int nsub = B * krrn_cdiv(HW, 16);
+  const dim3 grid(min(krrn_cdiv(nsub, kX3Waves), 256 * 2));
   hipStream_t s = (hipStream_t)stream;
-  const int vec = (HW % 4 == 0) && krrn_aligned16(out) ? 1 : 0;
-#define KRRN_1X1X3(NTV)                                                                                        \
-  if (nt == NTV) {                                                                                             \
-    const hipError_t e = hipFuncSetAttribute((const void*)conv1x1_nchw_x3_kernel<NTV>,                         \
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
-    if (e != hipSuccess) return (int)e;                                                                        \
-    hipLaunchKernelGGL(conv1x1_nchw_x3_kernel<NTV>, grid, dim3(64 * NTV), lds, s, in, in_cs, in_co, B, HW,     \
-                       reinterpret_cast<const unsigned*>(w3), n_store, scale, bias, out, out_cs, out_co, vec); \
-    return krrn_launch_status();                                                                               \
+#define KRRN_1X1X3(NTV)                                                                                      \
+  if (nt == NTV) {                                                                                           \
+    hipLaunchKernelGGL(conv1x1_nchw_x3_kernel<NTV>, grid, dim3(64 * kX3Waves), 0, s, in, in_cs, in_co, B, HW, \
+                       reinterpret_cast<const unsigned*>(w3), n_store, scale, bias, out, out_cs, out_co);     \
+    return krrn_launch_status();                                                                             \
   }
-  KRRN_1X1X3(1) KRRN_1X1X3(2) KRRN_1X1X3(3) KRRN_1X1X3(4) KRRN_1X1X3(5)
+  KRRN_1X1X3(3) KRRN_1X1X3(4) KRRN_1X1X3(5)
 #undef KRRN_1X1X3
   return KRRN_ESHAPE;
 }
@@ -303,6 +367,20 @@ KRRN_API int krrn_conv1x1_nchw_f32(const float* in, int in_cs, int in_co, int B,
   if (!krrn_aligned16(in) || !krrn_aligned16(wt)) return KRRN_EALIGN;
   if (out_co + n_store > out_cs || (long long)B * HW * in_cs >= (1LL << 40)) return KRRN_ESHAPE;
   if (cin > 256 || (long long)B * krrn_cdiv(HW, kPx) > 0x7fffffffLL) return KRRN_ESHAPE;  // kMaxU float4 per thread
+  if (N <= 4 && cin % 32 == 0 && cin <= 128) {  // the narrow (normal) head: VALU dot products, HBM-bound
+    const int nch = B * krrn_cdiv(HW, kNarrowPx);
+    const dim3 grid(min(krrn_cdiv(nch, 4), 256 * 3));
+    const int vec = (HW % 4 == 0) && krrn_aligned16(out) ? 1 : 0;
+    hipStream_t s = (hipStream_t)stream;
+#define KRRN_1X1N(KQ)                                                                                      \
+  if (cin == 32 * KQ) {                                                                                    \
+    hipLaunchKernelGGL(conv1x1_nchw_narrow_kernel<KQ>, grid, dim3(256), 0, s, in, in_cs, in_co, B, HW, wt, \
+                       N, n_store, scale, bias, out, out_cs, out_co, vec);                                 \
+    return krrn_launch_status();                                                                           \
+  }
+    KRRN_1X1N(1) KRRN_1X1N(2) KRRN_1X1N(4)
+#undef KRRN_1X1N
+  }
   const int Kp = (cin + 15) / 16 * 16;
   const int nt = (N + 15) / 16;
   const size_t lds = sizeof(float) * (size_t)(kPx + 16 * nt) * (Kp + 4);

@@ -363,7 +363,10 @@ def test_conv_small_group(dev):
 
 @pytest.mark.parametrize("B,HW,cin,cout,co,oc,Cx", [(3, 1000, 128, 72, 0, 0, 72), (2, 777, 128, 3, 0, 0, 3),
                                                    (4, 64, 20, 40, 4, 5, 50), (1, 130, 256, 80, 0, 0, 80),
-                                                   (2, 1000, 128, 9, 0, 3, 12)])
+                                                   (2, 1000, 128, 9, 0, 3, 12),
+                                                   # the narrow (N <= 4) form: cin 32 / 64 / 128, odd HW
+                                                   (3, 1000, 64, 2, 4, 1, 4), (2, 33, 32, 4, 0, 0, 4),
+                                                   (5, 4800, 128, 3, 0, 0, 3), (1, 31, 128, 1, 0, 2, 3)])
 def test_conv1x1_nchw(dev, B, HW, cin, cout, co, oc, Cx):
     """krrn_conv1x1_nchw_f32 (the heads' final 1x1 convs) vs torch fp32: ragged pixel tiles, K not a
     multiple of 16, channel-offset input and output."""
@@ -390,7 +393,7 @@ def test_conv1x1_nchw(dev, B, HW, cin, cout, co, oc, Cx):
         assert torch.isnan(out[:, :oc]).all()
 
 
-@pytest.mark.parametrize("B,HW,cout,co,oc,Cx", [(3, 1000, 72, 0, 0, 72), (2, 777, 72, 4, 0, 72), (4, 64, 20, 0, 5, 30),
+@pytest.mark.parametrize("B,HW,cout,co,oc,Cx", [(3, 1000, 72, 0, 0, 72), (2, 777, 72, 4, 0, 72), (4, 64, 40, 0, 5, 50),
                                                 (1, 130, 80, 0, 0, 80), (2, 1000, 50, 8, 3, 60), (2, 4, 72, 0, 0, 72),
                                                 (5, 4800, 72, 0, 0, 72)])
 def test_conv1x1_nchw_x3(dev, B, HW, cout, co, oc, Cx):
