@@ -336,13 +336,13 @@ KRRN_API int krrn_conv1x1_nchw_x3_f32(const float* in, int in_cs, int in_co, int
                                       int N, int n_store, const float* scale, const float* bias, float* out, int out_cs,
                                       int out_co, void* stream) {
   if (!in || !w3 || !out) return KRRN_EARG;
-  // 3..5 channel tiles: the staged pixel rows fit the registers of 3+ waves (two blocks per CU)
+  // 3..5 channel tiles (the weight LDS and the accumulators sized for them)
   if (B < 1 || HW < 1 || N <= 32 || N > 80 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
-  if (cin != 4 * kX3Q) return KRRN_ESHAPE;  // the heads' 128-channel input (weights in registers)
+  if (cin != 4 * kX3Q) return KRRN_ESHAPE;  // the heads' 128-channel input (8 k steps)
   if ((in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
   if (!krrn_aligned16(in) || !krrn_aligned16(w3)) return KRRN_EALIGN;
   if (out_co + n_store > out_cs || (long long)B * HW * in_cs >= (1LL << 40)) return KRRN_ESHAPE;
-  if ((long long)B * krrn_cdiv(HW, kPx) > 0x7fffffffLL) return KRRN_ESHAPE;
+  if ((long long)B * krrn_cdiv(HW, 16) > 0x3fffffffLL) return KRRN_ESHAPE;  // subtile index + grid stride fit int
   const int nt = (N + 15) / 16;
   const int nsub = B * krrn_cdiv(HW, 16);
   const dim3 grid(min(krrn_cdiv(nsub, kX3Waves), 256 * 2));

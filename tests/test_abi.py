@@ -57,5 +57,12 @@ def test_host_side_errors():
     # pnp: P < 5 -> KRRN_ESHAPE
     assert lib.krrn_pnp_ransac_f32(fake, 16, fake, 10, fake, 4, fake, fake, fake, fake, fake, fake, 10,
                                    ctypes.c_float(1.0), ctypes.c_double(0.9999), fake, fake, fake, fake, N, 1, N) == -2
+    # NCHW 1x1 split form: null weights -> KRRN_EARG; N outside (32, 80] or cin != 128 -> KRRN_ESHAPE;
+    # misaligned channel offset -> KRRN_EALIGN
+    nchw_x3 = lib.krrn_conv1x1_nchw_x3_f32
+    assert nchw_x3(fake, 128, 0, 1, 64, 128, N, 72, 72, N, N, fake, 72, 0, N) == -1
+    assert nchw_x3(fake, 128, 0, 1, 64, 128, fake, 16, 16, N, N, fake, 16, 0, N) == -2
+    assert nchw_x3(fake, 256, 0, 1, 64, 256, fake, 72, 72, N, N, fake, 72, 0, N) == -2
+    assert nchw_x3(fake, 136, 2, 1, 64, 128, fake, 72, 72, N, N, fake, 72, 0, N) == -3
     with pytest.raises(RuntimeError, match="KRRN_EARG"):
         _lib.check(-1, "x")
