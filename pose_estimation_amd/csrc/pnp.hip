@@ -764,12 +764,12 @@ __device__ void load_corr(int b, const float* xyz, int HW, const long long* choo
   }
 }
 
-// Phase 1: one RANSAC hypothesis per 16-lane group, 16 per block, grid (B, ceil(H / 16)). Writes the
+// Phase 1: one RANSAC hypothesis per 16-lane group, kHypPerBlock per block, grid (B, ceil(H / kHypPerBlock)). Writes the
 // f32 pose (R, t: the precision the inlier test uses) and the inlier count of every hypothesis. LDS:
 // the P correspondences only (5 KB at P = 256), so the blocks co-reside with the fusion / TBase
 // launches they run beside; no scratch memory (every register array has compile-time indices).
-constexpr int kHypPerBlock = 16;
-__global__ __launch_bounds__(256) void pnp_hyp_kernel(
+template <int kHypPerBlock>
+__global__ __launch_bounds__(16 * kHypPerBlock) void pnp_hyp_kernel(
     const float* __restrict__ xyz, int HW, const long long* __restrict__ choose, int N, const int* __restrict__ sel,
     int P, const float* __restrict__ xmap, const float* __restrict__ ymap, const float* __restrict__ K4,
     const double* __restrict__ extent, const double* __restrict__ lfb, const int* __restrict__ subsets, int H,
@@ -911,8 +911,18 @@ KRRN_API int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choo
   hipStream_t s = (hipStream_t)stream;
   float* hyp_pose = workspace;
   int* hyp_cnt = reinterpret_cast<int*>(workspace + (size_t)B * H * 12);
-  hipLaunchKernelGGL(pnp_hyp_kernel, dim3(B, krrn_cdiv(H, kHypPerBlock)), dim3(256), sizeof(float) * 5 * (size_t)P, s,
-                     xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
+  // hypotheses per block: 4 (one wave) leaves no idle tail groups at H = 100 and schedules at wave
+  // granularity (occupancy is one wave per SIMD either way); 16 = the round-2 4-wave blocks
+  static const int hpb = [] {
+    const char* e = getenv("KRRN_PNP_HPB");
+    return e && atoi(e) == 16 ? 16 : 4;
+  }();
+  if (hpb == 16)
+    hipLaunchKernelGGL(pnp_hyp_kernel<16>, dim3(B, krrn_cdiv(H, 16)), dim3(256), sizeof(float) * 5 * (size_t)P, s,
+                       xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
+  else
+    hipLaunchKernelGGL(pnp_hyp_kernel<4>, dim3(B, krrn_cdiv(H, 4)), dim3(64), sizeof(float) * 5 * (size_t)P, s,
+                       xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
   hipLaunchKernelGGL(pnp_refine_kernel, dim3(B), dim3(64), 0, s, xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent,
                      lfborder, H, thr, conf, hyp_pose, hyp_cnt, R, t, inliers, inlier_mask);
   return krrn_launch_status();
