@@ -194,8 +194,8 @@ __global__ __launch_bounds__(64 * kX3Waves) __attribute__((amdgpu_waves_per_eu(4
   };
   const int stride = gridDim.x * kX3Waves;
   int c = blockIdx.x * kX3Waves + wave;
-  // xr[st]: this subtile's quad of step st; once split, the register takes the next subtile's quad
-  // (in flight for a whole subtile of MFMAs)
+  // xr[st]: this subtile's quad of step st; once steps 2j and 2j + 1 are split, their registers take
+  // the next subtile's quads (in flight for a whole subtile of MFMAs)
   f32x4 xr[kX3Steps];
   if (c < nsub) {
     bool ok;
@@ -218,7 +218,10 @@ __global__ __launch_bounds__(64 * kX3Waves) __attribute__((amdgpu_waves_per_eu(4
       asm volatile("" : "+v"(wl_off));
       nx_u32x4 x0, x1;
       nx_split(xr[st], x0, x1);
-      if (more) xr[st] = nok ? *reinterpret_cast<const f32x4*>(np + 16 * st) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (more && (st & 1)) {  // steps 2j, 2j + 1 are the two halves of one 128-B line: request them together
+        xr[st - 1] = nok ? *reinterpret_cast<const f32x4*>(np + 16 * (st - 1)) : f32x4{0.f, 0.f, 0.f, 0.f};
+        xr[st] = nok ? *reinterpret_cast<const f32x4*>(np + 16 * st) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
       const nx_u32x4 xhm = nx_u32x4{x0[0], x0[1], x1[0], x1[1]};
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
