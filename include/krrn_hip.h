@@ -32,7 +32,7 @@ extern "C" {
 #define KRRN_EARG (-1)
 #define KRRN_ESHAPE (-2)
 #define KRRN_EALIGN (-3)
-#define KRRN_EUNSUPPORTED (-4) /* the vendor library (hipBLASLt) rejected the problem */
+#define KRRN_EUNSUPPORTED (-4) /* hipBLASLt rejected the problem, or a form the kernel does not offer */
 
 /* Implicit-GEMM convolution / GEMM on the f32 matrix cores, BN folded into scale/bias.
  * Replaces nn.Conv2d + BatchNorm2d (+ residual add) (+ ReLU) of BasicBlock / Bottleneck /
@@ -167,7 +167,8 @@ int krrn_basic_block_x3_f32(const float* in, int in_cs, int in_co, int B, int H,
  * Split-bf16 operands at f32 accuracy; each wave keeps its 32 activation rows in registers and
  * walks 32-column tiles. wpf holds W split into per-wave fragments (ops.gemm_weights_panel:
  * [N/32][K/8][3][64 lanes][4] u32). K = 64 or 128, N % 32 == 0, lda % 4 == 0, A / wpf 16-byte
- * aligned; `csplit` column ranges per row panel (grid = ceil(M / 128) x csplit). */
+ * aligned; `csplit` column ranges per row panel (grid = ceil(M / 128) x csplit). K = 128 with a
+ * residual: KRRN_EUNSUPPORTED. */
 int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N, const void* wpf, const float* bias,
                            const float* res, int ldr, float* out, int ldo, int relu, int csplit, void* stream);
 

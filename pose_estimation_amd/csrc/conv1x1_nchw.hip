@@ -187,6 +187,8 @@ __global__ __launch_bounds__(64 * kX3Waves) __attribute__((amdgpu_waves_per_eu(4
   }
   __syncthreads();
   const int spi = krrn_cdiv(HW, 16), nsub = B * spi;
+  const __amdgpu_buffer_rsrc_t rso =
+      __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, (int)((long long)B * out_cs * HW * 4), 0x00020000);
   auto x_ptr = [&](int c, bool& ok) {
     const int b = c / spi, px = (c - b * spi) * 16 + fr;
     ok = px < HW;
@@ -233,16 +235,20 @@ __global__ __launch_bounds__(64 * kX3Waves) __attribute__((amdgpu_waves_per_eu(4
         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nx_op(wmh), nx_op(x1), acc[t], 0, 0, 0);
       }
     }
-    // acc[t][i] = (channel 16 t + 4 g + i, pixel 16 (c % spi) + fr): 64-B NCHW runs per channel
+    // acc[t][i] = (channel 16 t + 4 g + i, pixel 16 (c % spi) + fr): 64-B NCHW runs per channel.
+    // Buffer stores: the lane's channel-group / pixel part in one 32-bit voffset, the (t, i) channel
+    // part (16 t + i) HW in the scalar offset -- with plain 64-bit addresses LLVM hoisted all 20
+    // per-channel offsets out of the subtile loop (40 VGPRs) and spilled 28 B / lane to scratch.
     const int b = c / spi, px = (c - b * spi) * 16 + fr;
     if (px < HW) {
-      float* ob = out + ((long long)b * out_cs + out_co) * HW + px;
+      const unsigned vo = (unsigned)((((b * out_cs + out_co) + 4 * g) * HW + px) * 4);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int n = 16 * t + 4 * g + i;
-          if (n < n_store) ob[(long long)n * HW] = acc[t][i] * ssc[n] + sbi[n];
+          if (n < n_store)
+            __builtin_amdgcn_raw_buffer_store_b32(acc[t][i] * ssc[n] + sbi[n], rso, vo, (16 * t + i) * HW * 4, 0);
         }
     }
   }
@@ -346,6 +352,7 @@ KRRN_API int krrn_conv1x1_nchw_x3_f32(const float* in, int in_cs, int in_co, int
   if (!krrn_aligned16(in) || !krrn_aligned16(w3)) return KRRN_EALIGN;
   if (out_co + n_store > out_cs || (long long)B * HW * in_cs >= (1LL << 40)) return KRRN_ESHAPE;
   if ((long long)B * krrn_cdiv(HW, 16) > 0x3fffffffLL) return KRRN_ESHAPE;  // subtile index + grid stride fit int
+  if ((long long)B * out_cs * HW * 4 >= 0x7FFFFFFFLL) return KRRN_ESHAPE;      // 32-bit buffer-store offsets
   const int nt = (N + 15) / 16;
   const int nsub = B * krrn_cdiv(HW, 16);
   const dim3 grid(min(krrn_cdiv(nsub, kX3Waves), 256 * 2));

@@ -255,9 +255,11 @@ KRRN_API int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N
       if (form == 2) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 1>), grid, dim3(512), 0, s, g);
       else if (form == 3) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 2>), grid, dim3(512), 0, s, g);
       else hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 0>), grid, dim3(512), 0, s, g);
-    } else if (K == 128) {  // residual at K = 128 does not fit the register budget: the form below
-      const dim3 grid0((unsigned)krrn_cdiv(M, 128), (unsigned)krrn_cdiv(ntiles, per));
-      hipLaunchKernelGGL(gemm_panel_x3_kernel<128>, grid0, dim3(256), 0, s, g);
+    } else if (K == 128) {
+      // a residual at K = 128 does not fit the LDS form's register budget; the register-only form
+      // that has room for it gave gather-conv outputs differing from the serial run beside the
+      // gather-conv and stays a diagnostic (KRRN_PANEL_FORM=0)
+      return KRRN_EUNSUPPORTED;
     } else if (res) {
       hipLaunchKernelGGL((gemm_plds_x3_kernel<64, true, 0>), grid, dim3(512), 0, s, g);
     } else {

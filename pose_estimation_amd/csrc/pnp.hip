@@ -544,9 +544,11 @@ __device__ __forceinline__ void kabsch(const double (&H)[9], double (&R)[9]) {
 }
 
 // R, t from betas (lane r holds component r of the 4 null-space vectors: vq); returns the mean
-// reprojection error.
+// reprojection error. Forced inline like epnp below: as real calls (the compiler's choice for
+// functions this size) their struct / array arguments went through the stack, 216 B of scratch
+// per lane of the hypothesis kernel, written once per hypothesis.
 template <class SUM>
-__device__ double r_and_t(const SUM& sum, const double (&vq)[4], const double (&betas)[4], const double cws[4][3],
+__device__ __forceinline__ double r_and_t(const SUM& sum, const double (&vq)[4], const double (&betas)[4], const double cws[4][3],
                           const double* ci, const double* cw, const Cam& cam, double (&R)[9], double (&t)[3]) {
   const int base = (threadIdx.x & 63) & ~15;
   double cr = 0.0;
@@ -602,7 +604,7 @@ __device__ double r_and_t(const SUM& sum, const double (&vq)[4], const double (&
 // L matrix and of every 6 x N least-squares system one per lane, the 12 x 12 eigen-solve shared
 // (eig12_rows). Result R (row-major), t, identical in every lane of the group.
 template <class SUM>
-__device__ void epnp(const SUM& sum, const Cam& cam, double (&Rout)[9], double (&tout)[3]) {
+__device__ __forceinline__ void epnp(const SUM& sum, const Cam& cam, double (&Rout)[9], double (&tout)[3]) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63, r = lane & 15, base = lane & ~15;
   const int n = sum.count();

@@ -255,8 +255,9 @@ class _Builder:
 
     def emit_gemm(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool) -> bool:
         """A wide 1x1 / stride-1 conv (layer1's Bottleneck projections, myhrnet.py:66-103) is a plain
-        GEMM over the NHWC rows: hipBLASLt through add_gemm (BN folded, residual + ReLU epilogue).
-        False (nothing emitted) when the layout or hipBLASLt does not fit."""
+        GEMM over the NHWC rows through add_gemm's own kernels (BN folded, residual + ReLU epilogue).
+        False (nothing emitted) when none fits -- layer1's 256 -> 64 projections (K = 256, N = 64):
+        they then run on the split-bf16 implicit GEMM (emit_conv), not on hipBLASLt."""
         if not (spec.kind == "conv" and spec.ksize == 1 and spec.stride == 1 and out.co == 0
                 and (res is None or res.co == 0)):
             return False
@@ -264,7 +265,7 @@ class _Builder:
         return add_gemm(self.plan, a=x.t, a_off=x.co, lda=x.cs, M=x.B * x.H * x.W, wt=spec.wt[0], K=spec.cin_p,
                         N=np_, scale=spec.scale, bias=spec.bias, out=out.t, ldo=out.cs, relu=relu,
                         res=res.t if res is not None else None, ldr=res.cs if res is not None else 0,
-                        cin=spec.cin, cout=spec.cout, tag="conv1x1_gemm")
+                        cin=spec.cin, cout=spec.cout, tag="conv1x1_gemm", blas_ok=False)
 
     @staticmethod
     def small_problem(x: Act, spec, out: Act, res: Optional[Act], relu: bool) -> dict:

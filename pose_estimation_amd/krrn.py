@@ -265,10 +265,13 @@ class KRRNPlan:
             return
         cur = torch.cuda.current_stream(self.plan.device)
         cur.synchronize()
+        before = torch.cuda.memory_reserved(self.plan.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.plan.run(self.env, serial=False)
         self.graph = g
+        # the captured graph's own pool counts against the plan budget too
+        self.nbytes += max(0, torch.cuda.memory_reserved(self.plan.device) - before)
         g.replay()
 
     def outputs(self, model: "KRRN") -> Dict[str, Optional[torch.Tensor]]:
@@ -284,10 +287,32 @@ class KRRNPlan:
 
 
 def plan_bytes(plan) -> int:
-    """Device bytes a Plan's workspaces hold (its keep-alive tensors)."""
+    """Device bytes a Plan's keep-alive objects hold: its workspaces and every tensor nested in
+    the lists / tuples / dicts / holder objects it keeps (folded and split weight planes, BN
+    vectors), each storage counted once."""
     if plan is None:
         return 0
-    return sum(t.numel() * t.element_size() for t in plan.buffers if isinstance(t, torch.Tensor))
+    seen, total = set(), 0
+    stack = list(plan.buffers)
+    visited = set()
+    while stack:
+        x = stack.pop()
+        if id(x) in visited:
+            continue
+        visited.add(id(x))
+        if isinstance(x, torch.Tensor):
+            if x.is_cuda:
+                st = x.untyped_storage()
+                if st.data_ptr() not in seen:
+                    seen.add(st.data_ptr())
+                    total += st.nbytes()
+        elif isinstance(x, (list, tuple)):
+            stack.extend(x)
+        elif isinstance(x, dict):
+            stack.extend(x.values())
+        elif hasattr(x, "__dict__") and not isinstance(x, type):
+            stack.extend(v for v in vars(x).values() if isinstance(v, (torch.Tensor, list, tuple, dict)))
+    return total
 
 
 PLAN_BUDGET = int(float(os.environ.get("KRRN_PLAN_BUDGET_GB", "48")) * (1 << 30))

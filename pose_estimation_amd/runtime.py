@@ -453,19 +453,23 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
              scale: Optional[torch.Tensor], bias: Optional[torch.Tensor], out: torch.Tensor, ldo: int, relu: bool,
              res: Optional[torch.Tensor] = None, ldr: int = 0, batch: int = 1, a_grp: int = 0, o_grp: int = 0,
              r_grp: int = 0, cin: Optional[int] = None, cout: Optional[int] = None, tag: str = "gemm",
-             require_x3: bool = False) -> bool:
+             require_x3: bool = False, blas_ok: bool = True) -> bool:
     """Append a plain GEMM out[m, n] = act(scale[n] * (A[m] . wt[n]) + bias[n] (+ res[m, n])) on hipBLASLt
     (krrn_blas_gemm_*; scale folded into the weights). Returns False when hipBLASLt is disabled
     (KRRN_BLAS=0) or rejects the problem: the caller then emits its own kernel. Short-K GEMMs go to
     the A-stationary split-bf16 kernel and K >= 256 ones to gemm_x3 first (own kernels).
-    require_x3: only gemm_x3 will do (its ldr = 0 per-group row broadcast); False if ineligible."""
+    require_x3: only gemm_x3 will do (its ldr = 0 per-group row broadcast); False if ineligible.
+    blas_ok=False: own kernels only (False instead of a hipBLASLt plan).
+    A K = 128 GEMM with a residual is not taken by the panel kernel: its register-only form (the only
+    one with room for the residual at K = 128) is kept for diagnostics."""
     dev = plan.device
     w = wt.reshape(N, -1)[:, :K].float()
     if scale is not None:
         w = w * scale.reshape(N, 1).to(w.device)
     w = w.contiguous()
     flops = 2.0 * (cin or K) * (cout or N) * M * batch
-    if GEMM_PANEL and not require_x3 and K in (64, 128) and N % 32 == 0 and batch == 1 and lda % 4 == 0 and a_off % 4 == 0:
+    if GEMM_PANEL and not require_x3 and K in (64, 128) and N % 32 == 0 and batch == 1 and lda % 4 == 0 \
+            and a_off % 4 == 0 and not (K == 128 and res is not None):
         wp = ops.gemm_weights_panel(w)
         plan.buffers.append([wp, bias])
         rows = (M + 255) // 256  # 256-row blocks, one per CU (96 KB of LDS each)
@@ -488,7 +492,7 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
                  meta=dict(kernel="gemm_x3", flops=flops, tag=tag, M=M * batch, N=N, K=K, splits=1,
                            mfma_flops=2.0 * M * batch * N * K * 6 / 16, mfma_bf16_flops=2.0 * M * batch * N * K * 6))
         return True
-    if not BLAS or require_x3:
+    if not BLAS or require_x3 or not blas_ok:
         return False
     h = ctypes.c_void_p()
     wsb = ctypes.c_longlong()

@@ -1,0 +1,123 @@
+"""Where does the wrong F0 of the cross-graph mismatch come from?
+
+The round-3 finding: with the two-slot pipeline's stage graphs replayed side by side
+(KRRN_STREAMS=1), F0 (the level-0 Conv_surface output) of slot 0 differed from a serial re-run in
+65-98 points while its inputs were bit-identical at the end. Two mechanisms fit: the surface conv
+produced the wrong values (it read something stale), or a store from elsewhere overwrote F0 after
+it was produced. This script tells them apart: right after each branch's surface conv, a copy op on
+the same stream writes that F0 slice into a shadow buffer (the value as produced). After a graph
+half-step:
+  shadow == serial, F0 != serial  -> F0 was overwritten after it was produced;
+  shadow != serial                 -> the surface conv itself produced wrong values (or a store
+                                      landed between it and the copy).
+It also reports the wrong entries' values against zero and against the other slot's F0 (the two
+slots load different batches here, so a value read across slots is recognisable).
+
+usage (GPU box): KRRN_STREAMS=1 python3 profiles/f0_shadow.py [REPS] [--history]"""
+import os
+import sys
+
+os.environ.setdefault("KRRN_STREAMS", "1")
+import torch  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from pose_estimation_amd import KRRN, make_config  # noqa: E402
+from pose_estimation_amd.pipeline import PipelinedPipeline, _sub_plan  # noqa: E402
+from pose_estimation_amd.runtime import Late, Op, P, ptr, _skey  # noqa: E402
+from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+REPS = int(args[0]) if args else 5
+dev = torch.device("cuda", 0)
+print(f"KRRN_STREAMS={os.environ['KRRN_STREAMS']}", flush=True)
+if "--history" in sys.argv:
+    # the history under which tests/test_gpu_pipeline.py::test_pipelined_graph_benched_shape failed:
+    # the file's other tests first, in order (as profiles/race_bench_shape.py)
+    import test_gpu_pipeline as tgp  # noqa: E402
+    for name, a in (("test_pipeline_matches_api_and_graph", (1,)), ("test_pipeline_matches_api_and_graph", (2,)),
+                    ("test_pipelined_matches_plain", ("backbone",)), ("test_pipelined_matches_plain", ("heads",)),
+                    ("test_pipelined_matches_plain", ("pose",)),
+                    ("test_pipelined_matches_plain_after_history", ("heads",)),
+                    ("test_pipelined_matches_plain_after_history", ("backbone",))):
+        try:
+            getattr(tgp, name)(dev, *a)
+            print(f"{name}{a}: ok", flush=True)
+        except AssertionError as e:
+            print(f"{name}{a}: MISMATCH {str(e)[:120]}", flush=True)
+    torch.cuda.synchronize()
+B, S, N = 64, 120, 1000
+m = KRRN(cfg=make_config(num_cls=1, backbone="w18"))
+init_weights(m, 0)
+m = m.to(dev).eval()
+pp = PipelinedPipeline(m, B, S, N, dev, seed=0, split="heads")
+for si, sl in enumerate(pp.slots):
+    sl.load(make_batch(B, S, N, seed=1 + si))
+
+# shadow copies right after each surface conv (krrn_gcn_conv_f32 with Y == NULL) of both slots
+shadows = []
+for si, sl in enumerate(pp.slots):
+    kp = sl.parts[0].kp
+    F0 = kp.fusion_bufs["F0"]
+    sh = torch.zeros_like(F0)
+    kp.plan.buffers.append(sh)
+    shadows.append(sh)
+    ops = kp.plan.ops
+    i = 0
+    while i < len(ops):
+        op = ops[i]
+        if isinstance(op, Op) and op.name == "krrn_gcn_conv_f32" and op.args[10].value is None:
+            out = op.args[14].value
+            co = (out - F0.data_ptr()) // 4
+            cp = Op("krrn_add_relu_f32", [P(F0.data_ptr() + 4 * co), 384, 0, P(0), 0, 0, P(sh.data_ptr() + 4 * co), 384,
+                                          0, B * N, 128, 0, Late(_skey(op.sid))], sid=op.sid)
+            ops.insert(i + 1, cp)
+            i += 1
+        i += 1
+# the stage views were cut before the insertion: rebuild them
+for si, sl in enumerate(pp.slots):
+    kp = sl.parts[0].kp
+    cut = kp.heads_end
+    pp.stage_a[si] = [(_sub_plan(kp.plan, 0, cut), kp.env)]
+    pp.stage_b[si] = [(kp.device_perm_plan, {}), (_sub_plan(kp.plan, cut, len(kp.plan.ops)), kp.env),
+                      (sl.parts[0].pose, {})]
+s0 = [sl.parts[0].kp.seed.clone() for sl in pp.slots]
+pp.run()
+torch.cuda.synchronize()
+pp.capture()
+F0s = [sl.parts[0].kp.fusion_bufs["F0"] for sl in pp.slots]
+bad_reps = 0
+for rep in range(REPS):
+    for sl, s in zip(pp.slots, s0):
+        sl.parts[0].kp.seed.copy_(s)
+    pp.reset()
+    pp.step()  # B(0) beside A(1)
+    torch.cuda.synchronize()
+    f0g, shg, f01 = F0s[0].clone(), shadows[0].clone(), F0s[1].clone()
+    pp.slots[0].parts[0].kp.seed.copy_(s0[0])
+    pp._run_b(0)  # serial re-run of slot 0's stage B from the same state
+    torch.cuda.synchronize()
+    f0s = F0s[0].clone()
+    d_f0 = (f0g != f0s)
+    d_sh = (shg != f0s)
+    print(f"rep {rep}: F0(graph) != F0(serial) at {int(d_f0.sum())} entries / {int(d_f0.any(-1).sum())} points; "
+          f"shadow(graph) != F0(serial) at {int(d_sh.sum())} entries; shadow != F0(graph) at "
+          f"{int((shg != f0g).sum())}", flush=True)
+    if d_f0.any() or d_sh.any():
+        bad_reps += 1
+        dd = d_f0 | d_sh
+        for sl3 in range(3):
+            part = dd[..., 128 * sl3:128 * (sl3 + 1)]
+            pts = part.any(-1).nonzero()
+            print(f"   slice {sl3}: {int(part.sum())} entries, {len(pts)} points, first (crop, point) "
+                  f"{pts[:6].tolist()}", flush=True)
+        idx = dd.nonzero()[:12]
+        for b, n, c in idx.tolist():
+            print(f"   [{b},{n},{c}] serial {float(f0s[b, n, c]):+.6e} graph {float(f0g[b, n, c]):+.6e} "
+                  f"shadow {float(shg[b, n, c]):+.6e} slot1 {float(f01[b, n, c]):+.6e}", flush=True)
+        wrong = f0g[d_f0]
+        if wrong.numel():
+            print(f"   wrong F0 values: zero {int((wrong == 0).sum())} of {wrong.numel()}; equal to slot-1 F0 "
+                  f"{int((f0g[d_f0] == f01[d_f0]).sum())}", flush=True)
+print(f"{bad_reps} of {REPS} half-steps mismatched", flush=True)

@@ -48,14 +48,27 @@ def main(path, out=None):
         else:
             cur = 0
     seg = ks[best[0]:best[1]]
+    # crop the window to whole forwards: from the first forward's opening kernel (one
+    # nchw_to_nhwc launch opens every forward plan) to the last step's closing kernel (the rng
+    # advance ends every bench step; pnp_refine the forward + pose plan): a window that opens or
+    # closes mid-forward would otherwise count a partial forward as a whole one (round-3 summary:
+    # 3 "forwards" for ~2.1 steps of kernels)
+    heads = [i for i, k in enumerate(seg) if k[2] == "nchw_to_nhwc_kernel"]
+    for tail_name in ("advance_kernel", "pnp_refine_kernel", "tbase_tail_kernel"):
+        tails = [i for i, k in enumerate(seg) if k[2] == tail_name]
+        if heads and tails and tails[-1] > heads[0]:
+            last = tails[-1]
+            nfw = sum(1 for i in heads if i <= last)
+            seg = seg[heads[0]:last + 1]
+            break
+    else:
+        nfw = max(1, len(heads))
     per = defaultdict(lambda: [0.0, 0])
     for s, e, n, q in seg:
         per[n][0] += (e - s) / 1e3
         per[n][1] += 1
     tot = sum(v[0] for v in per.values())
-    # serial plans (round 3) make the eager warm-up passes serial too, so the window can hold
-    # several forwards: one nchw_to_nhwc launch opens every forward plan
-    nsteps = max(1, per.get("nchw_to_nhwc_kernel", [0, 1])[1])
+    nsteps = max(1, nfw)
     res = {"serial_pass_kernels": len(seg), "serial_pass_busy_us": round(tot, 1), "forwards_in_window": nsteps,
            "busy_us_per_forward": round(tot / nsteps, 1),
            "serial_pass_span_us": round((seg[-1][1] - seg[0][0]) / 1e3, 1) if seg else 0,

@@ -91,7 +91,8 @@ def _run_panel(A, a_off, lda, M, K, N, W, bias, res, ldr, out, ldo, relu, csplit
 @pytest.mark.parametrize("M,K,N,lda,a_off,relu,with_res,csplit", [
     (1000, 128, 1024, 384, 128, False, False, 1),  # GCN level-0/1 shape: a branch slice of the 384-wide rows
     (1000, 128, 1024, 384, 256, False, False, 4),  # column ranges (level 1 fills the chip this way)
-    (77, 128, 96, 132, 4, True, True, 2),          # row tail (one partial panel), residual, ReLU, ragged split
+    (77, 128, 96, 132, 4, True, False, 2),         # row tail (one partial panel), ReLU, ragged split
+    (77, 64, 96, 132, 4, True, True, 2),           # the same with a residual (K = 64)
     (3000, 64, 256, 64, 0, True, True, 1)])        # layer1's 64 -> 256 1x1 (residual + ReLU)
 def test_gemm_panel_vs_torch(dev, M, K, N, lda, a_off, relu, with_res, csplit):
     """krrn_gemm_panel_x3_f32 (A-stationary split-bf16 GEMM, gemm_panel.hip) vs torch f64 / f32."""
@@ -130,6 +131,10 @@ def test_gemm_panel_rejects(dev):
     assert L.krrn_gemm_panel_x3_f32(P(A.data_ptr() + 4), 128, 64, 128, 128, ptr(wp), P(0), P(0), 0, ptr(out), 128, 0,
                                     1, s) < 0
     assert L.krrn_gemm_panel_x3_f32(P(0), 128, 64, 128, 128, ptr(wp), P(0), P(0), 0, ptr(out), 128, 0, 1, s) < 0
+    # K = 128 with a residual: only the register-only form has room for it, and that form is
+    # diagnostics-only: refused
+    assert L.krrn_gemm_panel_x3_f32(ptr(A), 128, 64, 128, 128, ptr(wp), P(0), ptr(out), 128, ptr(out), 128, 0, 1,
+                                    s) == -4
 
 
 def test_gemm_x3_group_row_bias(dev):
