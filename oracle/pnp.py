@@ -64,6 +64,27 @@ def pnp_ransac(obj, img, K4, subsets, thr=1.0, conf=0.9999):
     return R.reshape(3, 3), t, cnt, mask.astype(bool), best.value
 
 
+def pnp_ransac_cv(obj, img, K4, subsets, thr=1.0, conf=0.9999):
+    """pnp_ransac with the OpenCV-semantics EPnP of pnp_ref.c (cyclic 12 x 12 Jacobi, SVD beta
+    solves, QR Gauss-Newton, U V^T with the det fix): numerics independent of the kernel's.
+    Returns (R [3,3] f32, t [3] f32, inlier_count, best_h)."""
+    obj = np.ascontiguousarray(obj, dtype=np.float32)
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    K4 = np.ascontiguousarray(K4, dtype=np.float32)
+    subsets = np.ascontiguousarray(subsets, dtype=np.int32)
+    R = np.zeros(9, np.float32)
+    t = np.zeros(3, np.float32)
+    best = ctypes.c_int(-1)
+    lib = _load()
+    lib.oracle_pnp_ransac_cv.restype = ctypes.c_int
+    lib.oracle_pnp_ransac_cv.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    cnt = lib.oracle_pnp_ransac_cv(_p(obj), _p(img), len(obj), _p(K4), _p(subsets), len(subsets), float(thr),
+                                   float(conf), _p(R), _p(t), ctypes.byref(best))
+    return R.reshape(3, 3), t, cnt, best.value
+
+
 def pnp_hypotheses(obj, img, K4, subsets, thr=1.0):
     """Diagnostics: every RANSAC hypothesis -> (R [H,3,3] f32, t [H,3] f32, counts [H])."""
     obj = np.ascontiguousarray(obj, dtype=np.float32)

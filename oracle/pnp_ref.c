@@ -680,3 +680,320 @@ int oracle_pnp_ransac(const float* obj, const float* img, int P, const float* K4
   for (int i = 0; i < 3; ++i) t_out[i] = (float)t[i];
   return best >= 0 ? best_cnt : 0;
 }
+
+/* ---------------- OpenCV-semantics EPnP (independent of the kernel's numerics) ----------------
+ * The restatement above mirrors csrc/pnp.hip operation for operation (Cholesky normal equations,
+ * the parallel-ordered 12x12 Jacobi, the kernel's summation orders), so it pins the kernel's
+ * arithmetic, not cv2's. This second path follows OpenCV's epnp.cpp structure instead, with its
+ * own numerics, and is compared with the kernel at loose tolerances (tests/test_gpu_pnp.py):
+ *   - M^T M eigen-decomposition by cyclic Jacobi on the full 12 x 12 (cvSVD of MtM);
+ *   - the beta approximations by the SVD pseudo-inverse (cvSolve(..., CV_SVD));
+ *   - Gauss-Newton steps by Householder QR (epnp.cpp qr_solve);
+ *   - R from the SVD of ABt as U V^T with OpenCV's det < 0 fix (negate the third row), not Kabsch;
+ *   - every point sum sequential. */
+
+/* min ||A x - b|| through the pseudo-inverse of A^T A's eigen-decomposition (singular values below
+ * 1e-12 of the largest dropped, as an SVD solve does) */
+static void lsq_svd(const double* A, int m, int n, const double* b, double* x) {
+  double AtA[25], Atb[5], w[5], V[25];
+  for (int i = 0; i < n; ++i) {
+    Atb[i] = 0.0;
+    for (int j = 0; j < n; ++j) AtA[i * n + j] = 0.0;
+  }
+  for (int k = 0; k < m; ++k)
+    for (int i = 0; i < n; ++i) {
+      for (int j = 0; j < n; ++j) AtA[i * n + j] += A[k * n + i] * A[k * n + j];
+      Atb[i] += A[k * n + i] * b[k];
+    }
+  jacobi_eig(AtA, n, w, V);
+  const double tol = (w[0] > 0 ? w[0] : 0.0) * 1e-24; /* (1e-12 sigma_max)^2 */
+  for (int j = 0; j < n; ++j) x[j] = 0.0;
+  for (int i = 0; i < n; ++i) {
+    if (!(w[i] > tol)) continue;
+    double proj = 0.0;
+    for (int k = 0; k < n; ++k) proj += V[i * n + k] * Atb[k];
+    proj /= w[i];
+    for (int k = 0; k < n; ++k) x[k] += proj * V[i * n + k];
+  }
+}
+
+/* Householder QR least squares of the 6 x 4 Gauss-Newton system (epnp.cpp qr_solve) */
+static void qr_solve6x4(double* A, double* b, double* x) {
+  const int nr = 6, nc = 4;
+  double A1[4], A2[4];
+  for (int k = 0; k < nc; ++k) {
+    double eta = 0.0;
+    for (int i = k; i < nr; ++i) eta = fmax(eta, fabs(A[i * nc + k]));
+    if (eta == 0.0) { A1[k] = A2[k] = 0.0; continue; }
+    double sum = 0.0;
+    for (int i = k; i < nr; ++i) {
+      A[i * nc + k] /= eta;
+      sum += A[i * nc + k] * A[i * nc + k];
+    }
+    double sigma = sqrt(sum);
+    if (A[k * nc + k] < 0) sigma = -sigma;
+    A[k * nc + k] += sigma;
+    A1[k] = sigma * A[k * nc + k];
+    A2[k] = -eta * sigma;
+    for (int j = k + 1; j < nc; ++j) {
+      double s = 0.0;
+      for (int i = k; i < nr; ++i) s += A[i * nc + k] * A[i * nc + j];
+      const double tau = s / A1[k];
+      for (int i = k; i < nr; ++i) A[i * nc + j] -= tau * A[i * nc + k];
+    }
+  }
+  for (int j = 0; j < nc; ++j) {
+    if (A1[j] == 0.0) continue;
+    double tau = 0.0;
+    for (int i = j; i < nr; ++i) tau += A[i * nc + j] * b[i];
+    tau /= A1[j];
+    for (int i = j; i < nr; ++i) b[i] -= tau * A[i * nc + j];
+  }
+  for (int i = nc - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int j = i + 1; j < nc; ++j) s -= A[i * nc + j] * x[j];
+    x[i] = A2[i] != 0.0 ? s / A2[i] : 0.0;
+  }
+}
+
+static void gauss_newton_cv(const double* L, const double* rho, double betas[4]) {
+  for (int it = 0; it < 5; ++it) {
+    double A[24], b[6], x[4];
+    for (int i = 0; i < 6; ++i) {
+      const double* l = L + 10 * i;
+      double* a = A + 4 * i;
+      a[0] = 2 * l[0] * betas[0] + l[1] * betas[1] + l[3] * betas[2] + l[6] * betas[3];
+      a[1] = l[1] * betas[0] + 2 * l[2] * betas[1] + l[4] * betas[2] + l[7] * betas[3];
+      a[2] = l[3] * betas[0] + l[4] * betas[1] + 2 * l[5] * betas[2] + l[8] * betas[3];
+      a[3] = l[6] * betas[0] + l[7] * betas[1] + l[8] * betas[2] + 2 * l[9] * betas[3];
+      b[i] = rho[i] - (l[0] * betas[0] * betas[0] + l[1] * betas[0] * betas[1] + l[2] * betas[1] * betas[1] +
+                       l[3] * betas[0] * betas[2] + l[4] * betas[1] * betas[2] + l[5] * betas[2] * betas[2] +
+                       l[6] * betas[0] * betas[3] + l[7] * betas[1] * betas[3] + l[8] * betas[2] * betas[3] +
+                       l[9] * betas[3] * betas[3]);
+    }
+    qr_solve6x4(A, b, x);
+    for (int k = 0; k < 4; ++k) betas[k] += x[k];
+  }
+}
+
+/* epnp.cpp estimate_R_and_t: R = U V^T of ABt's SVD, third row negated when det(R) < 0 */
+static double r_and_t_cv(const double* ut, const double betas[4], const double* pw, const double* uv, int n,
+                         double cws[4][3], const double* ci, const double* cw, Cam cam, double* R, double* t) {
+  double ccs[4][3] = {{0}};
+  for (int i = 0; i < 4; ++i) {
+    const double* v = ut + 12 * (11 - i);
+    for (int j = 0; j < 4; ++j)
+      for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * v[3 * j + k];
+  }
+  double a0[4];
+  alphas_of(pw, cws, ci, a0);
+  const double z0 = a0[0] * ccs[0][2] + a0[1] * ccs[1][2] + a0[2] * ccs[2][2] + a0[3] * ccs[3][2];
+  const double sg = z0 < 0.0 ? -1.0 : 1.0;
+  double cc[3] = {0, 0, 0}, ABt[9] = {0};
+  for (int p = 0; p < n; ++p) {
+    double a[4];
+    alphas_of(pw + 3 * p, cws, ci, a);
+    for (int k = 0; k < 3; ++k) cc[k] += sg * (a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k]);
+  }
+  for (int k = 0; k < 3; ++k) cc[k] /= n;
+  for (int p = 0; p < n; ++p) {
+    double a[4], pc[3];
+    alphas_of(pw + 3 * p, cws, ci, a);
+    for (int k = 0; k < 3; ++k) pc[k] = sg * (a[0] * ccs[0][k] + a[1] * ccs[1][k] + a[2] * ccs[2][k] + a[3] * ccs[3][k]);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) ABt[3 * r + c] += (pc[r] - cc[r]) * (pw[3 * p + c] - cw[c]);
+  }
+  /* SVD ABt = U S V^T: V from eig(ABt^T ABt), U = ABt V / S (the third left vector completes U) */
+  double AtA[9], w[3], V[9], U[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) AtA[3 * i + j] = ABt[i] * ABt[j] + ABt[3 + i] * ABt[3 + j] + ABt[6 + i] * ABt[6 + j];
+  jacobi_eig(AtA, 3, w, V);
+  for (int i = 0; i < 3; ++i) {
+    double u[3];
+    for (int r = 0; r < 3; ++r) u[r] = ABt[3 * r] * V[3 * i] + ABt[3 * r + 1] * V[3 * i + 1] + ABt[3 * r + 2] * V[3 * i + 2];
+    double nr = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    if (i == 2 && nr < 1e-12 * sqrt(fmax(w[0], 0.0))) { /* rank 2: complete the left frame */
+      u[0] = U[1] * U[5] - U[2] * U[4];
+      u[1] = U[2] * U[3] - U[0] * U[5];
+      u[2] = U[0] * U[4] - U[1] * U[3];
+      nr = 1.0;
+    }
+    if (nr < 1e-300) nr = 1e-300;
+    for (int r = 0; r < 3; ++r) U[3 * i + r] = u[r] / nr;
+  }
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) R[3 * r + c] = U[r] * V[c] + U[3 + r] * V[3 + c] + U[6 + r] * V[6 + c];
+  const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                     R[2] * (R[3] * R[7] - R[4] * R[6]);
+  if (det < 0) {
+    R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8];
+  }
+  for (int r = 0; r < 3; ++r) t[r] = cc[r] - (R[3 * r] * cw[0] + R[3 * r + 1] * cw[1] + R[3 * r + 2] * cw[2]);
+  double err = 0.0;
+  for (int p = 0; p < n; ++p) {
+    const double* X = pw + 3 * p;
+    const double Xc = dot3(R, X) + t[0], Yc = dot3(R + 3, X) + t[1], Zc = dot3(R + 6, X) + t[2];
+    const double ue = cam.uc + cam.fu * Xc / Zc, ve = cam.vc + cam.fv * Yc / Zc;
+    const double du = uv[2 * p] - ue, dv = uv[2 * p + 1] - ve;
+    err += sqrt(du * du + dv * dv);
+  }
+  return err / n;
+}
+
+static double epnp_cv(const double* pw, const double* uv, int n, Cam cam, double* R, double* t) {
+  double cws[4][3], ci[9], cw[3];
+  ctrl_points(SUM_SEQ, pw, n, cws, ci, cw);
+  double MtM[144] = {0};
+  for (int p = 0; p < n; ++p) {
+    double a[4], r1[12], r2[12];
+    alphas_of(pw + 3 * p, cws, ci, a);
+    for (int j = 0; j < 4; ++j) {
+      r1[3 * j] = a[j] * cam.fu;
+      r1[3 * j + 1] = 0.0;
+      r1[3 * j + 2] = a[j] * (cam.uc - uv[2 * p]);
+      r2[3 * j] = 0.0;
+      r2[3 * j + 1] = a[j] * cam.fv;
+      r2[3 * j + 2] = a[j] * (cam.vc - uv[2 * p + 1]);
+    }
+    for (int i = 0; i < 12; ++i)
+      for (int j = 0; j < 12; ++j) MtM[i * 12 + j] += r1[i] * r1[j] + r2[i] * r2[j];
+  }
+  double w[12], ut[144];
+  jacobi_eig(MtM, 12, w, ut); /* rows of ut: eigenvectors, descending: rows 11..8 = the 4 smallest */
+  double L[60], rho[6];
+  {
+    const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
+    double dv[4][6][3];
+    for (int i = 0; i < 4; ++i) {
+      int a = 0, b = 1;
+      for (int j = 0; j < 6; ++j) {
+        for (int k = 0; k < 3; ++k) dv[i][j][k] = v[i][3 * a + k] - v[i][3 * b + k];
+        if (++b > 3) { ++a; b = a + 1; }
+      }
+    }
+    for (int i = 0; i < 6; ++i) {
+      double* r = L + 10 * i;
+      r[0] = dot3(dv[0][i], dv[0][i]);
+      r[1] = 2.0 * dot3(dv[0][i], dv[1][i]);
+      r[2] = dot3(dv[1][i], dv[1][i]);
+      r[3] = 2.0 * dot3(dv[0][i], dv[2][i]);
+      r[4] = 2.0 * dot3(dv[1][i], dv[2][i]);
+      r[5] = dot3(dv[2][i], dv[2][i]);
+      r[6] = 2.0 * dot3(dv[0][i], dv[3][i]);
+      r[7] = 2.0 * dot3(dv[1][i], dv[3][i]);
+      r[8] = 2.0 * dot3(dv[2][i], dv[3][i]);
+      r[9] = dot3(dv[3][i], dv[3][i]);
+    }
+    int a = 0, b = 1;
+    for (int j = 0; j < 6; ++j) {
+      const double d0 = cws[a][0] - cws[b][0], d1 = cws[a][1] - cws[b][1], d2 = cws[a][2] - cws[b][2];
+      rho[j] = d0 * d0 + d1 * d1 + d2 * d2;
+      if (++b > 3) { ++a; b = a + 1; }
+    }
+  }
+  double Rs[4][9], ts[4][3], errs[4], betas[4];
+  for (int approx = 1; approx <= 3; ++approx) {
+    const int nb = approx == 1 ? 4 : (approx == 2 ? 3 : 5);
+    static const int cols1[4] = {0, 1, 3, 6};
+    double A[30], x[5];
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < nb; ++j) A[nb * i + j] = L[10 * i + (approx == 1 ? cols1[j] : j)];
+    lsq_svd(A, 6, nb, rho, x);
+    if (approx == 1) {
+      if (x[0] < 0) {
+        betas[0] = sqrt(-x[0]);
+        for (int k = 1; k < 4; ++k) betas[k] = -x[k] / betas[0];
+      } else {
+        betas[0] = sqrt(x[0]);
+        for (int k = 1; k < 4; ++k) betas[k] = betas[0] > 0 ? x[k] / betas[0] : 0.0;
+      }
+    } else {
+      if (x[0] < 0) {
+        betas[0] = sqrt(-x[0]);
+        betas[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
+      } else {
+        betas[0] = sqrt(x[0]);
+        betas[1] = (x[2] > 0) ? sqrt(x[2]) : 0.0;
+      }
+      if (x[1] < 0) betas[0] = -betas[0];
+      betas[2] = approx == 3 && betas[0] != 0.0 ? x[3] / betas[0] : 0.0;
+      betas[3] = 0.0;
+    }
+    gauss_newton_cv(L, rho, betas);
+    errs[approx] = r_and_t_cv(ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[approx], ts[approx]);
+  }
+  int N = 1;
+  if (errs[2] < errs[1]) N = 2;
+  if (errs[3] < errs[N]) N = 3;
+  memcpy(R, Rs[N], sizeof(double) * 9);
+  memcpy(t, ts[N], sizeof(double) * 3);
+  return errs[N];
+}
+
+/* oracle_pnp_ransac with the OpenCV-semantics EPnP (same hypothesis subsets, inlier test and
+ * RANSAC loop; the refinement is EPnP on the best hypothesis' inliers, as solvePnPRansac does). */
+int oracle_pnp_ransac_cv(const float* obj, const float* img, int P, const float* K4, const int* subsets, int H,
+                         float thr, double conf, float* R_out, float* t_out, int* best_h) {
+  static double pw[3 * MAXP], uv[2 * MAXP];
+  Cam cam = {K4[0], K4[1], K4[2], K4[3]};
+  if (P > MAXP) P = MAXP;
+  int best = -1, best_cnt = 0, niters = H;
+  float bR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, bt[3] = {0, 0, 0};
+  const float thr2 = thr * thr;
+  for (int h = 0; h < niters; ++h) {
+    double spw[15], suv[10], R[9], t[3];
+    for (int i = 0; i < 5; ++i) {
+      const int id = subsets[5 * h + i];
+      for (int k = 0; k < 3; ++k) spw[3 * i + k] = obj[3 * id + k];
+      for (int k = 0; k < 2; ++k) suv[2 * i + k] = img[2 * id + k];
+    }
+    epnp_cv(spw, suv, 5, cam, R, t);
+    float Rf[9], tf[3];
+    for (int i = 0; i < 9; ++i) Rf[i] = (float)R[i];
+    for (int i = 0; i < 3; ++i) tf[i] = (float)t[i];
+    int cnt = 0;
+    for (int p = 0; p < P; ++p) {
+      const float X = obj[3 * p], Y = obj[3 * p + 1], Z = obj[3 * p + 2];
+      const float xc = Rf[0] * X + Rf[1] * Y + Rf[2] * Z + tf[0];
+      const float yc = Rf[3] * X + Rf[4] * Y + Rf[5] * Z + tf[1];
+      const float zc = Rf[6] * X + Rf[7] * Y + Rf[8] * Z + tf[2];
+      const float du = img[2 * p] - ((float)cam.fu * xc / zc + (float)cam.uc);
+      const float dv = img[2 * p + 1] - ((float)cam.fv * yc / zc + (float)cam.vc);
+      if (du * du + dv * dv <= thr2) ++cnt;
+    }
+    if (cnt > (best_cnt > 4 ? best_cnt : 4)) {
+      best_cnt = cnt;
+      best = h;
+      memcpy(bR, Rf, sizeof bR);
+      memcpy(bt, tf, sizeof bt);
+      niters = ransac_update_niters(conf, (double)(P - cnt) / P, 5, niters);
+    }
+  }
+  if (best_h) *best_h = best;
+  int n = 0;
+  for (int p = 0; p < P && best >= 0; ++p) {
+    const float X = obj[3 * p], Y = obj[3 * p + 1], Z = obj[3 * p + 2];
+    const float xc = bR[0] * X + bR[1] * Y + bR[2] * Z + bt[0];
+    const float yc = bR[3] * X + bR[4] * Y + bR[5] * Z + bt[1];
+    const float zc = bR[6] * X + bR[7] * Y + bR[8] * Z + bt[2];
+    const float du = img[2 * p] - ((float)cam.fu * xc / zc + (float)cam.uc);
+    const float dv = img[2 * p + 1] - ((float)cam.fv * yc / zc + (float)cam.vc);
+    if (du * du + dv * dv <= thr2) {
+      for (int k = 0; k < 3; ++k) pw[3 * n + k] = obj[3 * p + k];
+      for (int k = 0; k < 2; ++k) uv[2 * n + k] = img[2 * p + k];
+      ++n;
+    }
+  }
+  if (best >= 0 && n >= 5) {
+    double R[9], t[3];
+    epnp_cv(pw, uv, n, cam, R, t);
+    for (int i = 0; i < 9; ++i) bR[i] = (float)R[i];
+    for (int i = 0; i < 3; ++i) bt[i] = (float)t[i];
+  } else if (best < 0) {
+    for (int i = 0; i < 9; ++i) bR[i] = (i % 4 == 0) ? 1.f : 0.f;
+    for (int i = 0; i < 3; ++i) bt[i] = 0.f;
+  }
+  memcpy(R_out, bR, sizeof bR);
+  memcpy(t_out, bt, sizeof bt);
+  return best >= 0 ? best_cnt : 0;
+}
