@@ -210,6 +210,10 @@ int krrn_wino_variant(int v);
 int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* U3,
                              int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                              int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
+/* Kernel choice for krrn_conv3x3_wino_x3_f32 (process-wide; env KRRN_WINO_X3W): 0 = 32 output tiles
+ * x 64 channels per block at two waves per SIMD, 1 = 64 tiles x 64 channels per block at one wave per
+ * SIMD (accumulators in the AccVGPR file, half the weight bytes per MFMA). Bit-identical results. */
+int krrn_wino_x3_variant(int v);
 
 /* Direct conv for narrow layers: 3x3 / pad 1 / stride 1 or 2, or 1x1 / stride 1 (the HRNet
  * branches' BasicBlock convs, lib/network/hrnet/myhrnet.py:34-63, and the fuse layers' stride-2

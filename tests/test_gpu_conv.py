@@ -1,4 +1,6 @@
 """Implicit-GEMM conv kernel vs a plain PyTorch fp32 reference of the same op."""
+import os
+
 import pytest
 import torch
 import torch.nn as nn
@@ -266,15 +268,24 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     # the split-bf16 kernel: f32 accuracy (the f32 kernel's tolerance against torch, and within
     # f32 accumulation noise of the f32 kernel), every output written, pad channels zero
     U3 = ops.wino_weights_x3(U)
-    out.t.fill_(float("nan"))
-    out.t[..., np_:] = 0.0
-    _lib.check(L.krrn_conv3x3_wino_x3_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_, np_,
-                                          ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t), out.cs, 0,
-                                          1, P(torch.cuda.current_stream().cuda_stream)), "wino_x3")
-    torch.cuda.synchronize()
-    got3 = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
+    outs3 = []
+    try:
+        for variant in (0, 1):  # 32-tile two-waves-per-SIMD, 64-tile one-wave-per-SIMD
+            _lib.check(L.krrn_wino_x3_variant(variant), "krrn_wino_x3_variant")
+            out.t.fill_(float("nan"))
+            out.t[..., np_:] = 0.0
+            _lib.check(L.krrn_conv3x3_wino_x3_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_, np_,
+                                                  ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
+                                                  out.cs, 0, 1, P(torch.cuda.current_stream().cuda_stream)), "wino_x3")
+            torch.cuda.synchronize()
+            outs3.append(out.t.clone())
+    finally:
+        L.krrn_wino_x3_variant(int(os.environ.get("KRRN_WINO_X3W", "0")))
+    # the two split kernels: the same V / U operands and per-accumulator MFMA order, bit-identical
+    assert torch.equal(outs3[0], outs3[1])
+    got3 = outs3[0][..., :cout].permute(0, 3, 1, 2).cpu()
     torch.testing.assert_close(got3, ref, **TOL)
-    assert torch.count_nonzero(out.t[..., np_:]).item() == 0
+    assert torch.count_nonzero(outs3[0][..., np_:]).item() == 0
     scale = float(ref.abs().max())
     torch.testing.assert_close(got3, got, rtol=1e-5, atol=2e-6 * scale)
 
