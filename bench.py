@@ -89,16 +89,19 @@ def roofline_from_profile(prof, B: int):
                      **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {})}
                  for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])}
     traffic, tsrc = _pmc_traffic(dom)
-    # achieved = what the matrix pipe issues (for Winograd F(2x2,3x3) 2.25x fewer multiplies than the
-    # direct conv it replaces; for the split-bf16 Winograd the 6 bf16 term products per f32 product,
-    # against the bf16 peak), so frac <= 1 is a roofline fraction; the direct-conv-equivalent rate
-    # (SURVEY §8d's FLOP formula) is kept as `effective_tflops`
+    # achieved = ALGORITHMIC FLOPs per launch (SURVEY §8d's direct-conv formula 2 Cin Cout 9 M) /
+    # the average launch time, against the dense peak of the matrix pipe the kernel runs on (bf16 for
+    # the split kernels): the roofline fraction of the work. pipe_achieved / pipe_frac = what the
+    # matrix pipe actually issues (Winograd F(2x2,3x3): 16/36 of the direct multiplies; split-bf16:
+    # 6 bf16 term products per f32 product) -- pipe occupancy, not work
     bf16 = g["bf16"] > 0
     pipe_fl, peak = (g["bf16"], PEAK_BF16_MFMA_TFLOPS) if bf16 else (g["mfma"], PEAK_F32_MFMA_TFLOPS)
     mp = (pipe_fl / g["n"]) / (avg_ms * 1e-3) / 1e12 if pipe_fl > 0 else None
-    roof = {"kernel": dom, "bound": "mfma", "achieved": round(mp, 2) if mp else None,
+    roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
             "peak": peak, "unit": "TFLOP/s", "pipe": "bf16 (f32-accurate 3-term split)" if bf16 else "f32",
-            "frac": round(mp / peak, 4) if mp else None, "traffic": traffic,
+            "frac": round(achieved / peak, 4) if achieved else None,
+            "pipe_achieved": round(mp, 2) if mp else None, "pipe_frac": round(mp / peak, 4) if mp else None,
+            "traffic": traffic,
             "traffic_unit": "HBM bytes per launch", "traffic_source": tsrc,
             "launches": g["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
             "mfma_flops_per_launch": round(pipe_fl / g["n"]),

@@ -140,34 +140,14 @@ int krrn_gemm_x3_gather_f32(const int* ia, const float* A, long long a_bs, int a
                             long long a2_bs, int a2_st, int npts, int B, int K, int N, const void* w3f,
                             const float* bias, float* out, int ldo, int relu, void* stream);
 
-/* krrn_conv_small_f32 on the bf16 matrix cores at f32 accuracy (conv_small.hip, X3 form): the
- * staged input split into three exact bf16 terms, six term products per f32 product on
- * v_mfma_f32_16x16x32_bf16 (2.67x the f32 MFMA rate). w3: ops.quad_weights_x3 planes of the same
- * [N][taps * cin] weights; every other argument and check as krrn_conv_small_f32. */
-int krrn_conv_small_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* w3,
-                           int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
-                           int res_co, float* out, int out_cs, int out_co, int relu, int ksize, int stride, int nw,
-                           int ks, void* stream);
-
-/* One HRNet BasicBlock without downsample (conv_bb.hip; lib/network/hrnet/myhrnet.py:34-63):
- *   out = ReLU(s2 * conv3x3(ReLU(s1 * conv3x3(in) + b1)) + b2 + in)
- * on NHWC rows (channel stride / offset in_cs / in_co, out_cs / out_co; C padded channels, a
- * multiple of 4, pad channels zero), both convs stride 1 / pad 1 on the bf16 matrix cores at f32
- * accuracy (split operands), the intermediate kept in LDS. w1 / w2: ops.bb_weights_x3 planes;
- * s / b: [C] eval-BN scale / bias (16-byte aligned). T output rows per block (ops.bb_tile_rows);
- * in and out must not alias. */
-int krrn_basic_block_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int C, const void* w1,
-                            const float* s1, const float* b1, const void* w2, const float* s2, const float* b2,
-                            float* out, int out_cs, int out_co, int T, void* stream);
-
 /* Short-K GEMM streaming its output (gemm_panel.hip): the fusion's level-0 / level-1 GCN
  * `feature_map @ weights + bias` of Conv_layer (lib/network/point/gcn3d.py:136-164, K = 128,
  * N = 8 * 128) and layer1's 64 -> 256 1x1 convs (myhrnet.py:65-103, K = 64):
  *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n][k] + bias[n] + res[m*ldr + n]),  0 <= n < N
- * Split-bf16 operands at f32 accuracy; each wave keeps its 32 activation rows in registers and
- * walks 32-column tiles. wpf holds W split into per-wave fragments (ops.gemm_weights_panel:
- * [N/32][K/8][3][64 lanes][4] u32). K = 64 or 128, N % 32 == 0, lda % 4 == 0, A / wpf 16-byte
- * aligned; `csplit` column ranges per row panel (grid = ceil(M / 128) x csplit). K = 128 with a
+ * Split-bf16 operands at f32 accuracy; each wave keeps its 32 activation rows in registers, the
+ * 8 waves of a block walk 32-column tiles whose weights are staged once per block in LDS. wpf
+ * holds W split into per-wave fragments (ops.gemm_weights_panel: [N/32][K/8][3][64 lanes][4] u32). K = 64 or 128, N % 32 == 0, lda % 4 == 0, A / wpf 16-byte
+ * aligned; `csplit` column ranges per row panel (grid = ceil(M / 256) x csplit). K = 128 with a
  * residual: KRRN_EUNSUPPORTED. */
 int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N, const void* wpf, const float* bias,
                            const float* res, int ldr, float* out, int ldo, int relu, int csplit, void* stream);
@@ -196,10 +176,6 @@ int krrn_conv1x1_nchw_x3_f32(const float* in, int in_cs, int in_co, int B, int H
 int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const float* U,
                           int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                           int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
-/* Kernel choice for krrn_conv3x3_wino_f32 (process-wide; default 1, or env KRRN_WINO_V):
- * 1 = ring-staged raw patches, transform beside the MFMAs; 2 = the same without that overlap;
- * 0 = the register-staged V image. All three give bit-identical results. */
-int krrn_wino_variant(int v);
 /* krrn_conv3x3_wino_f32 on the bf16 matrix cores at f32 accuracy: every operand split into
  * three bf16 terms (x = x_h + x_m + x_l, round-to-nearest, exact), each product summed over the
  * six term pairs hh, hm, mh, hl, lh, mm (the dropped ones are below 2^-23 |a b|), accumulated in

@@ -45,11 +45,6 @@ struct SmallArgs {
   int M;                 // B * Ho * Wo
   int q;                 // channel quads per pixel (cin / 4)
   int pitch;             // LDS float4 per staged pixel: q rounded up to odd (conflict-free reads)
-  // split-bf16 form (X3): weights as planes [m h] [N16][kqp][4 u32] then [l] [N16][kqp][2 u32]
-  // (ops.quad_weights_x3), the staged input as two LDS planes [h h] / [m l] of plane_f4 slots each
-  const unsigned* w3;
-  int kqp;
-  int plane_f4;
 };
 
 constexpr unsigned kOOB = 0xFFFFFFF0u;
@@ -60,29 +55,7 @@ constexpr unsigned kOOB = 0xFFFFFFF0u;
 // is k-quad 4 st + g, i.e. tap (4 st + g) / q, channels 4 ((4 st + g) % q) .. +3, so a step can
 // straddle two taps and no channel padding is computed). With KS > 1 the K-slices' partial tiles
 // are summed through LDS in slice order (deterministic).
-typedef __bf16 cs_bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 cs_bf16x2 __attribute__((ext_vector_type(2)));
-typedef float cs_f32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned cs_u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned cs_u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ unsigned cs_pk(float a, float b) {
-  return __builtin_bit_cast(unsigned, __builtin_convertvector(cs_f32x2{a, b}, cs_bf16x2));  // RNE
-}
-// 4 channels -> the planes [h h] and [m l] (exact three-term split, as winograd.hip / conv_bb.hip)
-__device__ __forceinline__ void cs_split(const f32x4 x, cs_u32x4& p0, cs_u32x4& p1) {
-  const unsigned h0 = cs_pk(x[0], x[1]), h1 = cs_pk(x[2], x[3]);
-  const float r0 = x[0] - __builtin_bit_cast(float, h0 << 16), r1 = x[1] - __builtin_bit_cast(float, h0 & 0xFFFF0000u);
-  const float r2 = x[2] - __builtin_bit_cast(float, h1 << 16), r3 = x[3] - __builtin_bit_cast(float, h1 & 0xFFFF0000u);
-  const unsigned m0 = cs_pk(r0, r1), m1 = cs_pk(r2, r3);
-  const unsigned l0 = cs_pk(r0 - __builtin_bit_cast(float, m0 << 16), r1 - __builtin_bit_cast(float, m0 & 0xFFFF0000u));
-  const unsigned l1 = cs_pk(r2 - __builtin_bit_cast(float, m1 << 16), r3 - __builtin_bit_cast(float, m1 & 0xFFFF0000u));
-  p0 = cs_u32x4{h0, h1, h0, h1};
-  p1 = cs_u32x4{m0, m1, l0, l1};
-}
-__device__ __forceinline__ cs_bf16x8 cs_op(const cs_u32x4 v) { return __builtin_bit_cast(cs_bf16x8, v); }
-
-template <int NW, int KS, bool X3 = false>
+template <int NW, int KS>
 __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, float* slab) {
   constexpr int PM = 4 / KS;
   constexpr int kPixB = 16 * PM;
@@ -137,14 +110,7 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
 #pragma unroll
     for (int u = 0; u < kSU; ++u) {
       if (dst[u] < 0) continue;
-      if constexpr (X3) {
-        cs_u32x4 q0, q1;
-        cs_split(v[u], q0, q1);
-        *reinterpret_cast<cs_u32x4*>(slab + dst[u]) = q0;
-        *reinterpret_cast<cs_u32x4*>(slab + dst[u] + 4 * a.plane_f4) = q1;
-      } else {
-        *reinterpret_cast<f32x4*>(slab + dst[u]) = v[u];
-      }
+      *reinterpret_cast<f32x4*>(slab + dst[u]) = v[u];
     }
   }
 
@@ -194,74 +160,6 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
   // this lane's (tap, channel quad) at step s0, advanced by 4 quads per step
   int kq0 = 4 * s0 + g;
   int tap = kq0 / Q, c4 = kq0 - (kq0 / Q) * Q;
-  if constexpr (X3) {
-    // split-bf16: per step and 16-channel tile three v_mfma_f32_16x16x32_bf16 over the lane
-    // group's channel quad, W[h l] x X[h h] = hh + lh, W[m h] x X[h m] = mh + hm, W[m h] x X[m l]
-    // = mm + hl (2.67x the f32 MFMA rate; the dropped ml lm ll are below 2^-23 |w x|)
-    const long long nrec = (long long)((a.N + 15) / 16 * 16) * a.kqp;
-    const __amdgpu_buffer_rsrc_t rsMH = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.w3, (short)0, (int)min(nrec * 16, (long long)kOOB), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsL = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.w3 + nrec * 4), (short)0, (int)min(nrec * 8, (long long)kOOB), 0x00020000);
-    unsigned wr3[NW];
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-      const int n = n0 + 16 * j + fr;
-      wr3[j] = n < a.N ? (unsigned)(n * a.kqp + g) : kOOB;
-    }
-    constexpr int PF3 = 2;
-    cs_u32x4 wmh[PF3][NW];
-    cs_u32x2 wl[PF3][NW];
-    auto wload3 = [&](int st, int slot) {
-      const bool ok = st < s1;
-#pragma unroll
-      for (int j = 0; j < NW; ++j) {
-        const bool v = ok && wr3[j] != kOOB;
-        const unsigned r = v ? wr3[j] + (unsigned)(4 * st) : 0u;
-        wmh[slot][j] = __builtin_bit_cast(cs_u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsMH, v ? r * 16u : kOOB, 0, 0));
-        wl[slot][j] = __builtin_bit_cast(cs_u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsL, v ? r * 8u : kOOB, 0, 0));
-      }
-    };
-#pragma unroll
-    for (int u = 0; u < PF3; ++u) wload3(s0 + u, u);
-    const cs_u32x4* pl0 = reinterpret_cast<const cs_u32x4*>(slab);
-    const cs_u32x4* pl1 = pl0 + a.plane_f4;
-    for (int st0 = s0; st0 < s1; st0 += PF3) {
-#pragma unroll
-      for (int u = 0; u < PF3; ++u) {
-        const int st = st0 + u;
-        if (st >= s1) break;
-        cs_u32x4 cmh[NW];
-        cs_u32x2 cl[NW];
-#pragma unroll
-        for (int j = 0; j < NW; ++j) {
-          cmh[j] = wmh[u][j];
-          cl[j] = wl[u][j];
-        }
-        wload3(st + PF3, u);
-        const int t3 = tap + tb;
-        const int ty = t3 >= 6 ? 1 : (t3 >= 3 ? 0 : -1);
-        const int tx = t3 - 3 * (ty + 1) - 1;
-        const bool kok = tap < taps;
-        const int e = (kok ? base + ty * W2 + tx : base) * a.pitch + (kok ? c4 : 0);
-        cs_u32x4 x0 = pl0[e], x1 = pl1[e];
-        if (!kok) x0 = x1 = cs_u32x4{0u, 0u, 0u, 0u};
-        const cs_u32x4 xhm = cs_u32x4{x0[0], x0[1], x1[0], x1[1]};
-#pragma unroll
-        for (int j = 0; j < NW; ++j) {
-          const cs_u32x4 whl = cs_u32x4{cmh[j][2], cmh[j][3], cl[j][0], cl[j][1]};
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cs_op(whl), cs_op(x0), acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cs_op(cmh[j]), cs_op(xhm), acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cs_op(cmh[j]), cs_op(x1), acc[j], 0, 0, 0);
-        }
-        c4 += 4;
-        while (c4 >= Q) {
-          c4 -= Q;
-          ++tap;
-        }
-      }
-    }
-  } else {
 #ifndef KRRN_SMALL_PF
 #define KRRN_SMALL_PF 2
 #endif
@@ -312,7 +210,6 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
       }
     }
   }
-  }  // f32 form
 
   // ---- K-slice reduction through LDS (slice order: deterministic) ------------------------------
   if constexpr (KS > 1) {
@@ -350,10 +247,10 @@ __device__ __forceinline__ void small_body(const SmallArgs& a, int bx, int by, f
   }
 }
 
-template <int NW, int KS, bool X3 = false>
+template <int NW, int KS>
 __global__ __launch_bounds__(256) void conv_small_kernel(const SmallArgs a) {
   extern __shared__ __attribute__((aligned(16))) float slab[];
-  small_body<NW, KS, X3>(a, blockIdx.x, blockIdx.y, slab);
+  small_body<NW, KS>(a, blockIdx.x, blockIdx.y, slab);
 }
 
 // Up to 4 independent problems (the j-th BasicBlock conv of every HRNet branch) in one launch:
@@ -407,10 +304,9 @@ long long slab_floats(const SmallArgs& a, int pixb) {
   return worst * (a.W + 2 * a.pad) * a.pitch * 4;
 }
 
-// dynamic LDS bytes of one (NW, KS) launch: the slab (two planes in the split form), or the
-// K-slice partials if larger
-long long small_lds(const SmallArgs& a, int nw, int ks, bool x3 = false) {
-  long long lds = slab_floats(a, 64 / ks) * 4 * (x3 ? 2 : 1);
+// dynamic LDS bytes of one (NW, KS) launch: the slab, or the K-slice partials if larger
+long long small_lds(const SmallArgs& a, int nw, int ks) {
+  long long lds = slab_floats(a, 64 / ks) * 4;
   const long long red = 4LL * nw * 64 * 4 * 4;
   if (ks > 1 && lds < red) lds = red;
   return lds;
@@ -425,16 +321,14 @@ int set_lds(const void* fn, long long lds) {
   return KRRN_OK;
 }
 
-template <int NW, int KS, bool X3 = false>
-int small_launch(const SmallArgs& a0, hipStream_t s) {
+template <int NW, int KS>
+int small_launch(const SmallArgs& a, hipStream_t s) {
   constexpr int pixb = 64 / KS;
-  SmallArgs a = a0;
-  if (X3) a.plane_f4 = (int)(slab_floats(a, pixb) / 4);
-  const long long lds = small_lds(a, NW, KS, X3);
-  const int st = set_lds((const void*)conv_small_kernel<NW, KS, X3>, lds);
+  const long long lds = small_lds(a, NW, KS);
+  const int st = set_lds((const void*)conv_small_kernel<NW, KS>, lds);
   if (st != KRRN_OK) return st;
   const dim3 grid(krrn_cdiv(a.M, pixb), krrn_cdiv(krrn_cdiv(a.N, 16), NW));
-  hipLaunchKernelGGL((conv_small_kernel<NW, KS, X3>), grid, dim3(256), (size_t)lds, s, a);
+  hipLaunchKernelGGL((conv_small_kernel<NW, KS>), grid, dim3(256), (size_t)lds, s, a);
   return krrn_launch_status();
 }
 
@@ -466,9 +360,6 @@ int make_args(const float* in, int in_cs, int in_co, int B, int H, int W, int ci
   a.relu = relu; a.M = (int)M;
   a.q = cin / 4;
   a.pitch = a.q | 1;
-  a.w3 = nullptr;
-  a.kqp = krrn_cdiv(ksize * ksize * a.q, 4) * 4;
-  a.plane_f4 = 0;
   return KRRN_OK;
 }
 
@@ -489,28 +380,6 @@ KRRN_API int krrn_conv_small_f32(const float* in, int in_cs, int in_co, int B, i
   KRRN_SMALL(1, 2) KRRN_SMALL(2, 2) KRRN_SMALL(3, 2)
   KRRN_SMALL(1, 4) KRRN_SMALL(2, 4) KRRN_SMALL(3, 4)
 #undef KRRN_SMALL
-  return KRRN_EARG;
-}
-
-KRRN_API int krrn_conv_small_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
-                                    const void* w3, int N, int n_store, const float* scale, const float* bias,
-                                    const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
-                                    int relu, int ksize, int stride, int nw, int ks, void* stream) {
-  SmallArgs a;
-  if (!w3) return KRRN_EARG;
-  // make_args checks the f32 weight pointer too: any non-null placeholder, replaced below
-  const int st = make_args(in, in_cs, in_co, B, H, W, cin, reinterpret_cast<const float*>(w3), N, n_store, scale,
-                           bias, res, res_cs, res_co, out, out_cs, out_co, relu, ksize, stride, nw, ks, a);
-  if (st != KRRN_OK) return st;
-  a.w3 = reinterpret_cast<const unsigned*>(w3);
-  a.wt = nullptr;
-  hipStream_t s = (hipStream_t)stream;
-#define KRRN_SMALL3(NWV, KSV) \
-  if (nw == NWV && ks == KSV) return small_launch<NWV, KSV, true>(a, s);
-  KRRN_SMALL3(1, 1) KRRN_SMALL3(2, 1) KRRN_SMALL3(3, 1)
-  KRRN_SMALL3(1, 2) KRRN_SMALL3(2, 2) KRRN_SMALL3(3, 2)
-  KRRN_SMALL3(1, 4) KRRN_SMALL3(2, 4) KRRN_SMALL3(3, 4)
-#undef KRRN_SMALL3
   return KRRN_EARG;
 }
 

@@ -25,10 +25,11 @@
 // waves', so they skip LDS: 8 b128 loads per lane per chunk (1 KB contiguous per instruction),
 // one chunk ahead. One barrier per chunk. The output transform: wave w holds row u = w of every
 // (tile, channel)'s 4x4 M, so the column combination is lane-local and only 2 of 4 values per
-// row go through LDS; stores are float4 channel runs. The register-staged kernel
-// (wino_f23_kernel: every thread transforms one (tile, channel) patch into an LDS image of V,
-// weights staged through LDS, two barriers per chunk) stays selectable (krrn_wino_variant(0));
-// both give bit-identical outputs (same V operands, same MFMA order).
+// row go through LDS; stores are float4 channel runs. The step runs the split-bf16 forms below
+// (wino_f23_x3_kernel, wino_f23_x3w_kernel); this f32 kernel is their accuracy reference.
+// Round 1's register-staged kernel (every thread transforming one (tile, channel) patch into an
+// LDS image of V, weights staged through LDS, two barriers per chunk: bit-identical, 1.55 ms) and
+// the ring without the transform overlap were removed in round 4.
 // Measured (MI355X, 64 x 128 -> 128 x 120 x 120, profiles/bench_wino.py): staged 1.55 ms, ring
 // 1.41 ms (84 TF in the matrix pipe; 68 % MFMA-busy by SQ_VALU_MFMA_BUSY_CYCLES at 2.05 GHz,
 // waves 73 % issue-stalled, 10 % in s_waitcnt / barriers), ring without the transform overlap
@@ -45,17 +46,8 @@
 namespace {
 
 constexpr int kWT = 32;       // tiles per block
-#ifndef KRRN_WINO_A2
-#define KRRN_WINO_A2 0
-#endif
-#ifndef KRRN_WINO_FRAG2
-#define KRRN_WINO_FRAG2 0
-#endif
 #ifndef KRRN_WINO_EXP
 #define KRRN_WINO_EXP 0
-#endif
-#ifndef KRRN_WINO_SOUTER
-#define KRRN_WINO_SOUTER 0
 #endif
 #ifndef KRRN_WINO_WN
 #define KRRN_WINO_WN 64
@@ -63,10 +55,7 @@ constexpr int kWT = 32;       // tiles per block
 constexpr int kWN = KRRN_WINO_WN;  // output channels per block
 constexpr int kNJ = kWN / 32;      // 32-wide n-blocks per wave
 constexpr int kN4 = kWN / 4;       // 4-channel groups per tile
-constexpr int kNWF = 16 * kWN * 2 / 256;  // weight float4s staged per thread per chunk
-constexpr int kWBlocks = kWN == 64 ? 2 : 3;  // blocks per CU the LDS footprint allows
 constexpr int kWC = 8;        // input channels per chunk
-constexpr int kWP = kWC + 4;  // LDS row pitch (floats): 3 x 16 B
 constexpr unsigned kWOOB = 0xFFFF0000u;  // > any valid offset, and + channel offsets stays > it
 
 struct WinoArgs {
@@ -93,10 +82,7 @@ struct WinoArgs {
 // go through LDS ([u][c][tile][n], pitch kSP), and each thread then finishes the row
 // combination for 2 (tile, 4-channel) pairs and stores 2x2 pixels x float4.
 constexpr int kSP = kWN + 4;
-static_assert(4 * 2 * kWT * kSP <= 16 * (kWT + kWN) * kWP, "epilogue staging must fit the main-loop LDS");
 
-// ADD: accumulate into what another wave group staged at the same addresses (ping-pong kernel)
-template <bool ADD = false>
 __device__ __forceinline__ void wino_epi_put(float* smem, f32x16 (&acc)[4][kNJ]) {
   const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
   const int fr = lane & 31;
@@ -108,327 +94,13 @@ __device__ __forceinline__ void wino_epi_put(float* smem, f32x16 (&acc)[4][kNJ])
       const float m0 = acc[0][j][r], m1 = acc[1][j][r], m2 = acc[2][j][r], m3 = acc[3][j][r];
       float* p0 = smem + ((wave * 2 + 0) * kWT + row) * kSP + j * 32 + fr;
       float* p1 = smem + ((wave * 2 + 1) * kWT + row) * kSP + j * 32 + fr;
-      if (ADD) {
-        *p0 += m0 + m1 + m2;
-        *p1 += m1 - m2 - m3;
-      } else {
-        *p0 = m0 + m1 + m2;
-        *p1 = m1 - m2 - m3;
-      }
+      *p0 = m0 + m1 + m2;
+      *p1 = m1 - m2 - m3;
     }
 }
 
-__device__ __forceinline__ void wino_epi_stage(float* smem, f32x16 (&acc)[4][kNJ]) {
-  wino_epi_put(smem, acc);
-  __syncthreads();
-}
-
-template <int NT = 256>
-__device__ __forceinline__ void wino_epi_finish(const WinoArgs& a, const float* smem, int t0, int n0, int HWt) {
-  constexpr int kNP = kWT * kN4 / NT;  // (tile, 4-channel) pairs per thread
-  const int tid = threadIdx.x;
-  // geometry of this thread's (tile, 4-channel) pairs and their scale / bias
-  int pt[kNP], pn[kNP];
-  size_t ppix[kNP][4];
-  bool pok[kNP], qok[kNP][4];
-  f32x4 scl[kNP], bia[kNP];
-#pragma unroll
-  for (int i = 0; i < kNP; ++i) {
-    const int pr = tid + NT * i;
-    const int n4 = pr % kN4, tl = pr / kN4;
-    pt[i] = tl;
-    pn[i] = n0 + 4 * n4;
-    const int t = t0 + tl;
-    pok[i] = t < a.T && pn[i] < a.n_store;
-    const int tt = pok[i] ? t : 0;
-    const int b = tt / HWt;
-    const int rr = tt - b * HWt;
-    const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-      qok[i][q] = pok[i] && oy < a.H && ox < a.W;
-      ppix[i][q] = ((size_t)b * a.H + oy) * a.W + ox;
-    }
-    if (a.vec && pok[i]) {
-      const int n = pn[i];
-      scl[i] = a.scale ? *reinterpret_cast<const f32x4*>(a.scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
-      bia[i] = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < kNP; ++i) {
-    if (!pok[i]) continue;
-    const int tl = pt[i], n = pn[i];
-    const int n4 = (n - n0) >> 2;
-    f32x4 c[4][2];  // [u][c]
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) c[u][q] = *reinterpret_cast<const f32x4*>(smem + ((u * 2 + q) * kWT + tl) * kSP + 4 * n4);
-    f32x4 y[4];
-    y[0] = c[0][0] + c[1][0] + c[2][0];
-    y[1] = c[0][1] + c[1][1] + c[2][1];
-    y[2] = c[1][0] - c[2][0] - c[3][0];
-    y[3] = c[1][1] - c[2][1] - c[3][1];
-    if (a.vec) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!qok[i][q]) continue;
-        f32x4 v = y[q] * scl[i] + bia[i];
-        if (a.res) v += *reinterpret_cast<const f32x4*>(a.res + ppix[i][q] * a.res_cs + a.res_co + n);
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        *reinterpret_cast<f32x4*>(a.out + ppix[i][q] * a.out_cs + a.out_co + n) = v;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!qok[i][q]) continue;
-        const size_t pix = ppix[i][q];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (n + e >= a.n_store) break;
-          float v = y[q][e] * (a.scale ? a.scale[n + e] : 1.f) + (a.bias ? a.bias[n + e] : 0.f);
-          if (a.res) v += a.res[pix * a.res_cs + a.res_co + n + e];
-          if (a.relu) v = fmaxf(v, 0.f);
-          a.out[pix * a.out_cs + a.out_co + n + e] = v;
-        }
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ void wino_epilogue(const WinoArgs& a, float* smem, f32x16 (&acc)[4][kNJ], int t0, int n0,
-                                              int HWt) {
-  wino_epi_stage(smem, acc);
-  wino_epi_finish(a, smem, t0, n0, HWt);
-}
-
-// Staging of one 8-channel chunk: thread (tile st, channel sc) loads its 4x4 input patch
-// (raw buffer loads; out-of-image pixels and channels past cin return 0 = the conv's zero
-// padding) and 8 float4s of the chunk-major weights; stage() writes V = B^T d B and the
-// weights k-contiguous into LDS.
-struct WinoStager {
-  __amdgpu_buffer_rsrc_t rsA, rsU;
-  unsigned poff[16];  // byte offset of patch pixel (r, c), channel sc; kWOOB outside the image
-  unsigned woff[kNWF];  // byte offset of this thread's weight float4s at chunk 0
-  unsigned wstride;   // bytes per weight chunk
-  int st, sc, cin, nchunks;
-
-  int tid;  // thread index within the staging group (0..255)
-
-  __device__ __forceinline__ WinoStager(const WinoArgs& a, int t0, int n0, int HWt, int ltid) {
-    tid = ltid;
-    st = tid >> 3;
-    sc = tid & 7;
-    cin = a.cin;
-    nchunks = krrn_cdiv(a.cin, kWC);
-    const int b0 = min(t0, a.T - 1) / HWt;
-    const float* abase = a.in + (size_t)b0 * a.img + a.in_co;
-    const long long a_avail = ((long long)(a.B - b0) * a.img - a.in_co) * 4;
-    rsA = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, (int)min(a_avail, 0x7FFFFFFFLL), 0x00020000);
-    rsU = __builtin_amdgcn_make_buffer_rsrc((void*)a.U, (short)0,
-                                            (int)min((long long)nchunks * 16 * a.N * kWC * 4, 0x7FFFFFFFLL), 0x00020000);
-    const int t = t0 + st;
-    const bool ok = t < a.T;
-    const int tt = ok ? t : 0;
-    const int b = tt / HWt;
-    const int rr = tt - b * HWt;
-    const int ty = rr / a.Wt, tx = rr - (rr / a.Wt) * a.Wt;
-    const int iy0 = 2 * ty - 1, ix0 = 2 * tx - 1;
-    const long long pb = (long long)(b - b0) * a.img + sc;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int iy = iy0 + r, ix = ix0 + c;
-        const bool in = ok && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-        poff[4 * r + c] = in ? (unsigned)((pb + ((long long)iy * a.W + ix) * a.in_cs) * 4) : kWOOB;
-      }
-    // U is chunk-major [chunk][xi][N][8]: one chunk of one block is 16 contiguous 2 KB runs
-#pragma unroll
-    for (int i = 0; i < kNWF; ++i) {
-      const int e = tid + 256 * i;  // (xi, n, c4) over 16 x kWN x 2
-      const int xi = e / (2 * kWN), n = (e >> 1) % kWN, c4 = e & 1;
-      woff[i] = (n0 + n < a.N) ? (unsigned)((((long long)xi * a.N + n0 + n) * kWC + 4 * c4) * 4) : kWOOB;
-    }
-    wstride = (unsigned)(16 * a.N * kWC * 4);
-  }
-
-  // chunks past the last one load zeros (out-of-range buffer offsets), branch-free
-  __device__ __forceinline__ void load(int ck, float (&d)[16], f32x4 (&w)[kNWF]) const {
-    loadA(ck, d);
-    loadB(ck, w);
-  }
-
-  __device__ __forceinline__ void loadA(int ck, float (&d)[16]) const {
-    const int c0 = ck * kWC;
-    const unsigned cb = (unsigned)c0 * 4u;
-    const unsigned cmask = (c0 + sc < cin) ? 0u : kWOOB;
-#if KRRN_WINO_EXP == 1  // timing experiment: no input loads
-#pragma unroll
-    for (int p = 0; p < 16; ++p) d[p] = (float)(p + ck + sc);
-#else
-#pragma unroll
-    for (int p = 0; p < 16; ++p)
-      d[p] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsA, (poff[p] + cb) | cmask, 0, 0));
-#endif
-  }
-
-  __device__ __forceinline__ void loadB(int ck, f32x4 (&w)[kNWF]) const {
-    const unsigned wmask = (ck < nchunks) ? 0u : kWOOB;  // padded channels of the last chunk are zero in U
-    const unsigned wb = (unsigned)ck * wstride;
-#if KRRN_WINO_EXP == 2  // timing experiment: no weight loads
-#pragma unroll
-    for (int i = 0; i < kNWF; ++i) w[i] = f32x4{(float)ck, (float)i, 1.f, 2.f};
-#else
-#pragma unroll
-    for (int i = 0; i < kNWF; ++i)
-      w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsU, (woff[i] + wb) | wmask, 0, 0));
-#endif
-  }
-
-  __device__ __forceinline__ void stage(const float (&d)[16], const f32x4 (&w)[kNWF], float* As, float* Bs) const {
-    // V = B^T d B
-    float t[16];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
-      t[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
-      t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
-      t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      As[((u * 4 + 0) * kWT + st) * kWP + sc] = t[u * 4 + 0] - t[u * 4 + 2];
-      As[((u * 4 + 1) * kWT + st) * kWP + sc] = t[u * 4 + 1] + t[u * 4 + 2];
-      As[((u * 4 + 2) * kWT + st) * kWP + sc] = t[u * 4 + 2] - t[u * 4 + 1];
-      As[((u * 4 + 3) * kWT + st) * kWP + sc] = t[u * 4 + 1] - t[u * 4 + 3];
-    }
-#pragma unroll
-    for (int i = 0; i < kNWF; ++i) {
-      const int e = tid + 256 * i;
-      const int xi = e / (2 * kWN), n = (e >> 1) % kWN, c4 = e & 1;
-      *reinterpret_cast<f32x4*>(Bs + (xi * kWN + n) * kWP + 4 * c4) = w[i];
-    }
-  }
-};
-
-// Wave w owns components xi = 4w .. 4w+3 over the 32 x 64 block: per chunk 32 MFMAs (one
-// ds_read_b128 per operand feeds 4; the s-outer order with all 12 fragments live measured equal
-// and costs 36 VGPRs).
-__device__ __forceinline__ void wino_mma(const float* As, const float* Bs, f32x16 (&acc)[4][kNJ]) {
-  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
-  const int fr = lane & 31, fk = (lane >> 5) * 4;
-#if KRRN_WINO_FRAG2
-  // fragments of component x+1 are read while component x's 8 MFMAs issue (no exposed
-  // ds_read latency when the SIMD's other wave is not issuing MFMAs)
-  f32x4 av[2], bv[2][kNJ];
-  auto frag = [&](int x, int slot) {
-    const int xi = 4 * wave + x;
-    av[slot] = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
-#pragma unroll
-    for (int j = 0; j < kNJ; ++j)
-      bv[slot][j] = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
-  };
-  frag(0, 0);
-#pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    if (x + 1 < 4) frag(x + 1, (x + 1) & 1);
-#pragma unroll
-    for (int j = 0; j < kNJ; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[x & 1][s], bv[x & 1][j][s], acc[x][j], 0, 0, 0);
-  }
-  return;
-#endif
-#pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    const int xi = 4 * wave + x;
-    const f32x4 av = *reinterpret_cast<const f32x4*>(As + (xi * kWT + fr) * kWP + fk);
-#pragma unroll
-    for (int j = 0; j < kNJ; ++j) {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(Bs + (xi * kWN + j * 32 + fr) * kWP + fk);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-#if KRRN_WINO_EXP == 3  // timing experiment: no MFMAs
-        acc[x][j][s] += av[s] * bv[s];
-#else
-        acc[x][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[x][j], 0, 0, 0);
-#endif
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ void wino_block(const WinoArgs& a, int& t0, int& n0, int& HWt) {
-  const int n_tiles = krrn_cdiv(a.N, kWN);
-  const int bid = krrn_xcd_remap(blockIdx.x, krrn_cdiv(a.T, kWT) * n_tiles);
-  const int tb = bid / n_tiles, nb = bid % n_tiles;
-  t0 = tb * kWT;
-  n0 = nb * kWN;
-  HWt = a.Ht * a.Wt;
-}
-
-// Single LDS buffer (73.5 KB) -> 2 blocks per CU; one block's staging overlaps the
-// other's MFMAs, the next chunk's global loads are in flight during the current MFMAs.
-__global__ __launch_bounds__(256, kWBlocks) void wino_f23_kernel(const WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[16 * (kWT + kWN) * kWP];
-  float* As = smem;                   // [xi][tile][c]
-  float* Bs = smem + 16 * kWT * kWP;  // [xi][n][c]
-  int t0, n0, HWt;
-  wino_block(a, t0, n0, HWt);
-  const WinoStager sg(a, t0, n0, HWt, threadIdx.x);
-  f32x16 acc[4][kNJ];
-#pragma unroll
-  for (int x = 0; x < 4; ++x)
-#pragma unroll
-    for (int j = 0; j < kNJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[x][j][r] = 0.f;
-#if KRRN_WINO_A2
-  // input patches two chunks ahead (their loads miss L2 more often than the L2-resident weights)
-  float d0[16], d1[16];
-  f32x4 w[kNWF];
-  sg.loadA(0, d0);
-  sg.loadB(0, w);
-  sg.loadA(1, d1);
-  for (int ck = 0; ck < sg.nchunks; ck += 2) {
-    sg.stage(d0, w, As, Bs);
-    __syncthreads();
-    sg.loadB(ck + 1, w);
-    sg.loadA(ck + 2, d0);
-    wino_mma(As, Bs, acc);
-    __syncthreads();
-    if (ck + 1 >= sg.nchunks) break;
-    sg.stage(d1, w, As, Bs);
-    __syncthreads();
-    sg.loadB(ck + 2, w);
-    sg.loadA(ck + 3, d1);
-    wino_mma(As, Bs, acc);
-    __syncthreads();
-  }
-#else
-  float d[16];
-  f32x4 w[kNWF];
-  sg.load(0, d, w);
-  for (int ck = 0; ck < sg.nchunks; ++ck) {
-    sg.stage(d, w, As, Bs);
-    __syncthreads();
-    sg.load(ck + 1, d, w);  // in flight during the MFMAs (zeros past the last chunk)
-    wino_mma(As, Bs, acc);
-    __syncthreads();
-  }
-#endif
-  wino_epilogue(a, smem, acc, t0, n0, HWt);
-}
-
-// ---- Ring variant (KRRN_WINO_V=3): raw input patches through a 2-slot LDS ring, the
-// transform done by the consuming waves, weights straight to registers --------------------------
+// ---- The f32 ring kernel (krrn_conv3x3_wino_f32): raw input patches through a 3-slot LDS ring,
+// the transform done by the consuming waves, weights straight to registers ---------------------
 // Block = 16 x 2 output tiles (32 x 4 output pixels of one image) x 64 output channels; wave w
 // owns component row u = w (xi = 4w .. 4w+3) as above. Per 8-channel chunk the block stages the
 // RAW input region its 32 tiles read (6 rows x 34 cols x 8 channels = 408 16-B pieces, 2 per
@@ -499,7 +171,6 @@ __device__ __forceinline__ void wino_epi_finish2d(const WinoArgs& a, const float
   }
 }
 
-template <int PIPE>
 __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[4 * 2 * kWT * kSP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -594,15 +265,6 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
     V[3] = t[1] - t[3];
   };
   auto mma = [&](const f32x4 (&V)[4], const f32x4 (&wc)[4][kNJ]) {
-#if KRRN_WINO_SOUTER
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2)
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-#pragma unroll
-        for (int j = 0; j < kNJ; ++j)
-          acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(V[v][s2], wc[v][j][s2], acc[v][j], 0, 0, 0);
-#else
 #pragma unroll
     for (int v = 0; v < 4; ++v)
 #pragma unroll
@@ -610,32 +272,10 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2)
           acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(V[v][s2], wc[v][j][s2], acc[v][j], 0, 0, 0);
-#endif
   };
 
   f32x4 raw[2];
   f32x4 w[4][kNJ];
-  if constexpr (PIPE == 0) {
-    load_raw(0, raw);
-    load_w(0, w);
-    store_raw(0, raw);
-    load_raw(1, raw);
-    __syncthreads();
-    for (int ck = 0; ck < nck; ++ck) {
-      f32x4 V[4];
-      make_v(smem + (ck & 1) * kRSlot, V);
-      f32x4 wc[4][kNJ];
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-#pragma unroll
-        for (int j = 0; j < kNJ; ++j) wc[v][j] = w[v][j];
-      load_w(ck + 1, w);
-      mma(V, wc);
-      store_raw((ck + 1) & 1, raw);
-      load_raw(ck + 2, raw);
-      __syncthreads();
-    }
-  } else {
     // 3-slot ring: V of chunk ck+1 is formed (LDS reads + transform) beside chunk ck's MFMAs
     load_raw(0, raw);
     load_w(0, w);
@@ -663,7 +303,6 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
       for (int v = 0; v < 4; ++v) V[v] = Vn[v];
       __syncthreads();
     }
-  }
 #if KRRN_WINO_EXP == 4  // timing experiment: one store per lane instead of the epilogue
   float sum = 0.f;
 #pragma unroll
@@ -893,8 +532,8 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
 //     thread), 3 slots, one barrier per chunk; LDS slot of a piece = h * 484 + (col & 1) * 242 +
 //     row * 24 + col / 2 (16-B units): make_v's ds_read_b128 and the staging ds_write_b128 are
 //     bank-conflict-free (every lane group of the instruction hits 16 distinct 16-B bank slots);
-//   * weights: as the 32-tile kernel (plane U_mh b128 + plane U_l b64 per (v, n-block)), double
-//     buffered two chunks ahead, reloaded once both M-blocks used them;
+//   * weights: as the 32-tile kernel (plane U_mh b128 + plane U_l b64 per (v, n-block)), one
+//     buffer (48 VGPRs), component v's reloaded for the next chunk once both M-blocks used them;
 //   * epilogue: the column combination (c0, c1) of every (tile, channel) through LDS (139 KB, the
 //     ring's space), then rows combined with BN / residual / ReLU and float4 channel-run stores.
 // Same V operands, U operands and per-accumulator MFMA order as wino_f23_x3_kernel: bit-identical
@@ -1134,13 +773,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 
 }  // namespace
 
-// kernel choice (krrn_wino_variant): 1 = the ring kernel with the next chunk's transform beside
-// the MFMAs (default), 2 = the ring kernel without that overlap, 0 = the register-staged kernel
-static int g_wino_variant = [] {
-  const char* e = getenv("KRRN_WINO_V");
-  return e ? atoi(e) : 1;
-}();
-
 // split-bf16 kernel choice (krrn_wino_x3_variant): 0 = the 32-tile two-waves-per-SIMD kernel,
 // 1 = the 64-tile one-wave-per-SIMD kernel (wino_f23_x3w_kernel); env KRRN_WINO_X3W sets the start value
 static int g_wino_x3_variant = [] {
@@ -1151,12 +783,6 @@ static int g_wino_x3_variant = [] {
 KRRN_API int krrn_wino_x3_variant(int v) {
   if (v < 0 || v > 1) return KRRN_EARG;
   g_wino_x3_variant = v;
-  return KRRN_OK;
-}
-
-KRRN_API int krrn_wino_variant(int v) {
-  if (v < 0 || v > 2) return KRRN_EARG;
-  g_wino_variant = v;
   return KRRN_OK;
 }
 
@@ -1188,16 +814,9 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   if (span >= 0x7FFF0000LL || (long long)krrn_cdiv(cin, kWC) * 16 * N * kWC * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long blocks = (long long)krrn_cdiv(a.T, kWT) * krrn_cdiv(N, kWN);
   if (blocks > 0x7fffffffLL) return KRRN_ESHAPE;
-  if (g_wino_variant == 0) {
-    hipLaunchKernelGGL(wino_f23_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-  } else {
-    const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kWN);
-    if (rb > 0x7fffffffLL || a.img * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
-    if (g_wino_variant == 2)
-      hipLaunchKernelGGL(wino_f23_ring_kernel<0>, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
-    else
-      hipLaunchKernelGGL(wino_f23_ring_kernel<1>, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
-  }
+  const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kWN);
+  if (rb > 0x7fffffffLL || a.img * 4 >= 0x7FFF0000LL) return KRRN_ESHAPE;
+  hipLaunchKernelGGL(wino_f23_ring_kernel, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }
 

@@ -49,20 +49,6 @@ FUSE_ID_FIRST = os.environ.get("KRRN_FUSE_ID_FIRST", "1") == "1"
 WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
 # implicit-GEMM convs (transposed convs, stem / transitions) likewise (krrn_conv2d[_group]_x3_f32)
 CONV_X3 = os.environ.get("KRRN_CONV_X3", "1") == "1"
-# the HRNet branch BasicBlocks as one fused launch each (conv_bb.hip); KRRN_BB_T forces the rows
-# per block (0 = ops.bb_tile_rows). Off by default: measured slower in the step (DESIGN.md §3,
-# "Fused BasicBlock"): 12.81 vs 12.42 ms with the 20 / 36-channel branches fused, 13.43 with all
-BB_FUSED = os.environ.get("KRRN_BB", "0") == "1"
-# the small direct convs on split-bf16 operands (krrn_conv_small_x3_f32) instead of f32 MFMAs: off by
-# default, measured slower (profiles/bench_small.py X3=1: 24.4 / 14.1 / 14.1 / 16.2 vs 18.9 / 13.3 /
-# 13.2 / 14.2 us; step 5000 vs 5202 crops/s): the latency-bound K loop gains nothing from the faster
-# MFMAs and pays for the split staging, the doubled LDS slab and 1.5x the weight bytes
-SMALL_X3 = os.environ.get("KRRN_SMALL_X3", "0") == "1"
-BB_T = int(os.environ.get("KRRN_BB_T", "0"))
-# widest block (16-channel tiles) taken: the 72 / 144-channel branches measured no faster fused than
-# as two conv_small launches (profiles/bench_bb.py: their long K chains leave little MFMA work per
-# step to hide the weight latency), so they stay on conv_small
-BB_MAX_NTT = int(os.environ.get("KRRN_BB_MAX_NTT", "3"))
 
 BN_MOMENTUM = 0.1
 
@@ -285,13 +271,7 @@ class _Builder:
 
     def emit_small(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         p = self.small_problem(x, spec, out, res, relu)
-        name = "krrn_conv_small_f32"
-        if SMALL_X3:  # split-bf16 operands on the bf16 matrix cores (f32 accuracy)
-            w3 = ops.quad_weights_x3(spec.wt[0], p["N"], spec.ksize ** 2 * spec.cin_p)
-            self.specs.append(w3)
-            p["wt"] = ptr(w3)
-            name = "krrn_conv_small_x3_f32"
-        self.plan.add(name, p["x"], p["in_cs"], p["in_co"], p["B"], p["H"], p["W"], p["cin"], p["wt"],
+        self.plan.add("krrn_conv_small_f32", p["x"], p["in_cs"], p["in_co"], p["B"], p["H"], p["W"], p["cin"], p["wt"],
                       p["N"], p["n_store"], p["scale"], p["bias"], p["res"], p["res_cs"], p["res_co"], p["out"],
                       p["out_cs"], p["out_co"], p["relu"], p["ksize"], p["stride"], p["nw"], p["ks"],
                       meta=dict(kernel=f"conv_small<{p['nw']},{p['ks']}>", flops=p["flops"], tag=tag, M=p["M"], N=p["N"],
@@ -402,49 +382,9 @@ class _Builder:
 
     # -- blocks ------------------------------------------------------------------------
     def basic(self, x: Act, blk: BasicBlock, out: Optional[Act] = None) -> Act:
-        if BB_FUSED and blk.downsample is None:
-            y = self.emit_bb(x, blk, out)
-            if y is not None:
-                return y
         h = self.conv(x, blk.conv1, blk.bn1, relu=True)
         res = x if blk.downsample is None else self.conv(x, blk.downsample[0], blk.downsample[1])
         return self.conv(h, blk.conv2, blk.bn2, out=out, res=res, relu=True)
-
-    def emit_bb(self, x: Act, blk: BasicBlock, out: Optional[Act]) -> Optional[Act]:
-        """The whole BasicBlock as one krrn_basic_block_x3_f32 launch (conv1 + BN + ReLU, conv2 + BN
-        + residual + ReLU, intermediate in LDS) where both convs are narrow stride-1 3x3s the
-        small-conv path would run (the HRNet branch blocks); None (nothing emitted) otherwise."""
-        s1 = ops.make_conv(blk.conv1, blk.bn1, self.dev, cin_p=x.cp)
-        if not (s1.kind == "conv" and s1.ksize == 3 and s1.stride == 1 and s1.pad == 1 and s1.cout == x.c
-                and pad4(s1.cout) == x.cp and not ops.wino_eligible(s1, x.B * x.H * x.W)
-                and ops.small_conv_eligible(s1, x)):
-            return None
-        s2 = ops.make_conv(blk.conv2, blk.bn2, self.dev, cin_p=x.cp)
-        if not (s2.ksize == 3 and s2.stride == 1 and s2.pad == 1 and s2.cout == x.c):
-            return None
-        C = x.cp
-        if (C + 15) // 16 > BB_MAX_NTT:
-            return None
-        T = BB_T or ops.bb_tile_rows(x.B, x.H, x.W, C)
-        if T < 1:
-            return None
-        out = out if out is not None else self.act(x.H, x.W, x.c)
-        w1 = ops.bb_weights_x3(s1.wt[0], C)
-        w2 = ops.bb_weights_x3(s2.wt[0], C)
-        self.specs.extend([s1, s2, w1, w2])
-        M = x.B * x.H * x.W
-        ntt = (C + 15) // 16
-        kq = -(-(9 * C // 4) // 16) * 16
-        rows1 = x.B * sum(min(y0 + T + 1, x.H) - max(y0 - 1, 0) for y0 in range(0, x.H, T))
-        pix_tiles = x.B * sum(-(-((min(y0 + T + 1, x.H) - max(y0 - 1, 0)) * x.W) // 16)
-                              + -(-((min(y0 + T, x.H) - y0) * x.W) // 16) for y0 in range(0, x.H, T))
-        bf16 = 2.0 * 16 * (ntt * 16) * (kq * 4) * 6 * pix_tiles  # padded tiles the MFMAs issue
-        self.plan.add("krrn_basic_block_x3_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, C, ptr(w1), ptr(s1.scale),
-                      ptr(s1.bias), ptr(w2), ptr(s2.scale), ptr(s2.bias), ptr(out.t), out.cs, out.co, T,
-                      meta=dict(kernel="basic_block_x3", flops=2.0 * 2 * s1.cin * s1.cout * 9 * M, tag="hr_bb",
-                                M=M, N=C, K=9 * C, splits=1, rows1=rows1, T=T, mfma_flops=bf16 / 16,
-                                mfma_bf16_flops=bf16))
-        return out
 
     def bottleneck(self, x: Act, blk: Bottleneck) -> Act:
         h = self.conv(x, blk.conv1, blk.bn1, relu=True)

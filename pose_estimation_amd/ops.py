@@ -288,7 +288,7 @@ def gemm_weights_x3(wt: torch.Tensor) -> torch.Tensor:
 
 def quad_weights_x3(wt: torch.Tensor, N: int, K: int, kq_mult: int = 4) -> torch.Tensor:
     """Conv weights [>= N][>= K] f32 (k = tap * cin + c, ops.make_conv's packing) -> the split planes
-    the channel-quad kernels read (krrn_conv_small_x3_f32, krrn_basic_block_x3_f32), int32: the
+    the channel-quad kernels read (krrn_conv1x1_nchw_x3_f32), int32: the
     [m h] plane [N16][KQp][4] (per output channel and channel quad kq: m0..m3 h0..h3 bf16) then the
     [l] plane [N16][KQp][2] (l0..l3); N16 = N rounded up to 16, KQp = K / 4 rounded up to a
     multiple of kq_mult, zero padded (padding channels / quads contribute exact zeros)."""
@@ -301,30 +301,6 @@ def quad_weights_x3(wt: torch.Tensor, N: int, K: int, kq_mult: int = 4) -> torch
     mh = torch.cat([m, h], dim=-1).contiguous().view(torch.int32).reshape(-1)
     lp = l.contiguous().view(torch.int32).reshape(-1)
     return torch.cat([mh, lp]).contiguous()
-
-
-def bb_weights_x3(wt: torch.Tensor, C: int) -> torch.Tensor:
-    """A BasicBlock conv's weights [N >= C][9 C] -> krrn_basic_block_x3_f32's planes
-    (quad_weights_x3 with the quads padded to a multiple of 16: the kernel runs its reduction in
-    groups of 4 steps of 4 quads)."""
-    return quad_weights_x3(wt, C, 9 * C, kq_mult=16)
-
-
-def bb_tile_rows(B: int, H: int, W: int, C: int, max_lds: int = 160 * 1024) -> int:
-    """Output rows per block of krrn_basic_block_x3_f32: the T minimising the per-CU pixel-tile
-    work ceil(blocks / 256) * (conv1 + conv2 16-pixel tiles of a block), LDS within max_lds
-    (mirror of the kernel's bb_lds_bytes); ties -> larger T (fewer halo rows staged). 0 = none fits."""
-    qp = (C // 4) | 1
-    best, best_t = None, 0
-    for T in range(1, H + 1):
-        lds = 2 * (min(T + 4, H + 2) + min(T + 2, H + 2)) * (W + 2) * qp * 16
-        if lds > max_lds:
-            continue
-        blocks = B * (-(-H // T))
-        cost = -(-blocks // 256) * (-(-(min(T + 2, H) * W) // 16) + -(-(T * W) // 16)) + 2
-        if best is None or cost <= best:
-            best, best_t = cost, T
-    return best_t
 
 
 def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:

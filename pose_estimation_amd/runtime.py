@@ -48,7 +48,6 @@ _lib.register("krrn_conv2d_group_x3_f32", [P, I, I, P])
 _lib.register("krrn_conv2d_x3_f32", [P, I, I, I, I, I, I, I, I, I, I, P, P, P, I, I, P, P, P, I, P, I, I, P, I, I, I, I,
                                      I, I, I, I, I, I, I, P, P])
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
-_lib.register("krrn_wino_variant", [I])
 _lib.register("krrn_wino_x3_variant", [I])
 _lib.register("krrn_conv3x3_wino_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv1x1_nchw_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
@@ -59,8 +58,6 @@ _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])
 _lib.register("krrn_gemm_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, L, L, L, P])
-_lib.register("krrn_conv_small_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, I, I, I, I, P])
-_lib.register("krrn_basic_block_x3_f32", [P, I, I, I, I, I, I, P, P, P, P, P, P, P, I, I, I, P])
 _lib.register("krrn_gemm_x3_gather_f32", [P, P, L, I, P, P, L, I, I, I, I, I, P, P, P, I, I, P])
 _lib.register("krrn_gemm_panel_x3_f32", [P, I, I, I, I, P, P, P, I, P, I, I, I, P])
 

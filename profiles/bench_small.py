@@ -20,7 +20,7 @@ B = int(os.environ.get("B", 64))
 shapes = [(20, 30), (36, 15), (72, 8), (144, 4)]  # (padded C, side)
 L = _lib.lib()
 st = P(torch.cuda.current_stream().cuda_stream)
-tag = os.path.basename(os.environ.get("KRRN_HIP_LIB", "in-tree")) + (" x3" if os.environ.get("X3") == "1" else "")
+tag = os.path.basename(os.environ.get("KRRN_HIP_LIB", "in-tree"))
 for cp, H in shapes:
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, H, H, cp, generator=g).to(dev)
@@ -31,8 +31,7 @@ for cp, H in shapes:
     out = torch.zeros(B, H, H, cp, device=dev)
     nw, ks = ops.small_conv_config(B * H * H, (cp + 15) // 16, cp)
 
-    w3 = ops.quad_weights_x3(w, cp, 9 * cp)
-    fn, wp = (L.krrn_conv_small_x3_f32, w3) if os.environ.get("X3") == "1" else (L.krrn_conv_small_f32, w)
+    fn, wp = L.krrn_conv_small_f32, w
 
     def run():
         _lib.check(fn(ptr(x), cp, 0, B, H, H, cp, ptr(wp), cp, cp, ptr(sc), ptr(bi), ptr(res), cp, 0,
