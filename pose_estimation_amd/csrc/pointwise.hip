@@ -12,27 +12,6 @@
 
 namespace {
 
-// PyTorch's upsample_bilinear2d source index (aten/src/ATen/native/UpSample.h,
-// area_pixel_compute_source_index) evaluated in f32.
-__device__ __forceinline__ void src_index(int dst, int in_size, float scale, int align, int& i0, int& i1,
-                                          float& l0, float& l1) {
-  float s;
-  if (align) {
-    s = scale * (float)dst;
-  } else {
-    s = scale * ((float)dst + 0.5f) - 0.5f;
-    s = s < 0.f ? 0.f : s;
-  }
-  int i = (int)s;
-  i = i > in_size - 1 ? in_size - 1 : i;
-  i0 = i;
-  i1 = i + ((i < in_size - 1) ? 1 : 0);
-  float lam = s - (float)i;
-  lam = fminf(fmaxf(lam, 0.f), 1.f);
-  l1 = lam;
-  l0 = 1.f - lam;
-}
-
 // IT = the flat-index type: 32-bit whenever the launch fits (64-bit division is emulated and
 // dominated these memory-bound kernels)
 template <typename IT>
@@ -50,14 +29,14 @@ __global__ void resize_bilinear_kernel(const float* __restrict__ in, int Hi, int
   const int b = (int)(p / Ho);
   int y0, y1, x0, x1;
   float ly0, ly1, lx0, lx1;
-  src_index(oy, Hi, sh, align, y0, y1, ly0, ly1);
-  src_index(ox, Wi, sw, align, x0, x1, lx0, lx1);
+  krrn_src_index(oy, Hi, sh, align, y0, y1, ly0, ly1);
+  krrn_src_index(ox, Wi, sw, align, x0, x1, lx0, lx1);
   const float* ib = in + (long long)b * Hi * Wi * in_cs + in_co + 4 * c4;
   const f32x4 v00 = *reinterpret_cast<const f32x4*>(ib + ((long long)y0 * Wi + x0) * in_cs);
   const f32x4 v01 = *reinterpret_cast<const f32x4*>(ib + ((long long)y0 * Wi + x1) * in_cs);
   const f32x4 v10 = *reinterpret_cast<const f32x4*>(ib + ((long long)y1 * Wi + x0) * in_cs);
   const f32x4 v11 = *reinterpret_cast<const f32x4*>(ib + ((long long)y1 * Wi + x1) * in_cs);
-  f32x4 r = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+  f32x4 r = krrn_bilerp4(v00, v01, v10, v11, ly0, ly1, lx0, lx1);
   const long long opix = ((long long)b * Ho + oy) * Wo + ox;
   if (add) r = *reinterpret_cast<const f32x4*>(add + opix * add_cs + add_co + 4 * c4) + r;
   if (relu) {
@@ -88,8 +67,8 @@ __global__ void resize_up2x2_kernel(const float* __restrict__ in, int Hi, int Wi
   float ly0[2], ly1[2], lx0[2], lx1[2];
 #pragma unroll
   for (int d = 0; d < 2; ++d) {
-    src_index(min(2 * oy2 + d, Ho - 1), Hi, sh, align, y0[d], y1[d], ly0[d], ly1[d]);
-    src_index(min(2 * ox2 + d, Wo - 1), Wi, sw, align, x0[d], x1[d], lx0[d], lx1[d]);
+    krrn_src_index(min(2 * oy2 + d, Ho - 1), Hi, sh, align, y0[d], y1[d], ly0[d], ly1[d]);
+    krrn_src_index(min(2 * ox2 + d, Wo - 1), Wi, sw, align, x0[d], x1[d], lx0[d], lx1[d]);
   }
   const float* ib = in + (long long)b * Hi * Wi * in_cs + in_co + 4 * c4;
   f32x4 P[3][3];
@@ -117,7 +96,7 @@ __global__ void resize_up2x2_kernel(const float* __restrict__ in, int Hi, int Wi
       if (ox >= Wo) break;
       const int ca = x0[dx] - x0[0], cb = x1[dx] - x0[0];
       const f32x4 v00 = pick3(row0, ca), v01 = pick3(row0, cb), v10 = pick3(row1, ca), v11 = pick3(row1, cb);
-      f32x4 r = ly0[dy] * (lx0[dx] * v00 + lx1[dx] * v01) + ly1[dy] * (lx0[dx] * v10 + lx1[dx] * v11);
+      f32x4 r = krrn_bilerp4(v00, v01, v10, v11, ly0[dy], ly1[dy], lx0[dx], lx1[dx]);
       const long long opix = ((long long)b * Ho + oy) * Wo + ox;
       if (add) r = *reinterpret_cast<const f32x4*>(add + opix * add_cs + add_co + 4 * c4) + r;
       if (relu) {

@@ -74,6 +74,10 @@ struct WinoArgs {
   int relu;
   int vec;        // float4 epilogue (16-B aligned channel runs, n_store % 4 == 0)
   int Ht, Wt, T;  // tiles per column / row, total tiles
+  // fused x2 upsample (wino_f23_x3w_kernel<true>): `in` is the Hs x Ws source, H x W = 2Hs x 2Ws its
+  // align_corners=True bilinear upsample; img counts source-image elements
+  int Hs, Ws;
+  float sh, sw;
 };
 
 // Output transform Y = A^T M A + epilogue. Wave w holds row u = w of the 4x4 component grid
@@ -554,6 +558,13 @@ __device__ __forceinline__ int xw_slot(int h, int rr, int rc) {
   return h * kXHalfP + (rc & 1) * kXColP + rr * kXRowP + (rc >> 1);
 }
 
+// Source region of the fused-upsample form (UP2): the 10 x 34 up-sampled pixels of a block read at
+// most 7 x 19 source pixels (scale (Hs - 1) / (2 Hs - 1) < 1/2: 9 up rows span < 4.5 source rows, so
+// 6 distinct floor rows + the next one; 33 up columns < 16.5 source columns: 18 + 1).
+constexpr int kSR = 7, kSC = 19, kSPieces = kSR * kSC * 2, kSPer = (kSPieces + 255) / 256;
+static_assert(3 * kXSlot + 2 * kSPieces <= kXEpi / 4, "ring + source buffers fit the epilogue staging");
+
+template <bool UP2>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino_f23_x3w_kernel(
     const WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[kXEpi];
@@ -573,33 +584,103 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.in + (size_t)b * a.img + a.in_co), (short)0, (int)min(a.img * 4 - (long long)a.in_co * 4, 0x7FFFFFFFLL),
       0x00020000);
-  unsigned roff[kXPer], roffm[kXPer];  // roffm: the upper channel half masked (a last chunk of 4 channels)
-  int rdst[kXPer];                     // LDS 16-B slot in a ring slot, -1: no piece
+  int rdst[kXPer];  // LDS 16-B slot in a ring slot, -1: no piece
 #pragma unroll
   for (int k = 0; k < kXPer; ++k) {
     const int e = tid + 256 * k;
-    const int pix = e >> 1, hh = e & 1;
-    const int rr = pix / kXRC, rc = pix - (pix / kXRC) * kXRC;
-    const int iy = 2 * ty0 - 1 + rr, ix = 2 * tx0 - 1 + rc;
-    const bool ok = e < kXPieces && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    roff[k] = ok ? (unsigned)((((long long)iy * a.W + ix) * a.in_cs + 4 * hh) * 4) : kWOOB;
-    roffm[k] = hh ? kWOOB : roff[k];
-    rdst[k] = e < kXPieces ? xw_slot(hh, rr, rc) : -1;
+    rdst[k] = e < kXPieces ? xw_slot(e & 1, (e >> 1) / kXRC, (e >> 1) % kXRC) : -1;
   }
-  f32x4 raw[kXPer];
+  // !UP2: the raw pieces straight from the input image, loaded 3 chunks ahead
+  // UP2: the block's 7 x 19 SOURCE pixels of a chunk into a 2-slot LDS buffer, loaded 4 chunks
+  //      ahead; each up-sampled piece of the raw region is then blended from its 4 source pixels
+  //      (krrn_bilerp4: the expression of the resize kernels, bit-identical) into the ring slot
+  constexpr int kLPer = UP2 ? kSPer : kXPer;
+  unsigned roff[kLPer], roffm[kLPer];  // roffm: the upper channel half masked (a last chunk of 4 channels)
+  int sdst[kLPer];                     // UP2: 16-B slot in a source buffer, -1: no piece
+  int upk[UP2 ? kXPer : 1];            // UP2: packed source slots of an up piece (-1: outside the image)
+  float uwy[UP2 ? kXPer : 1], uwx[UP2 ? kXPer : 1];
+  if constexpr (!UP2) {
+#pragma unroll
+    for (int k = 0; k < kXPer; ++k) {
+      const int e = tid + 256 * k;
+      const int pix = e >> 1, hh = e & 1;
+      const int rr = pix / kXRC, rc = pix - (pix / kXRC) * kXRC;
+      const int iy = 2 * ty0 - 1 + rr, ix = 2 * tx0 - 1 + rc;
+      const bool ok = e < kXPieces && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      roff[k] = ok ? (unsigned)((((long long)iy * a.W + ix) * a.in_cs + 4 * hh) * 4) : kWOOB;
+      roffm[k] = hh ? kWOOB : roff[k];
+      sdst[k] = -1;
+    }
+  } else {
+    int sy0, sx0, i1;
+    float l0, l1;
+    krrn_src_index(max(2 * ty0 - 1, 0), a.Hs, a.sh, 1, sy0, i1, l0, l1);
+    krrn_src_index(max(2 * tx0 - 1, 0), a.Ws, a.sw, 1, sx0, i1, l0, l1);
+#pragma unroll
+    for (int k = 0; k < kSPer; ++k) {
+      const int e = tid + 256 * k;
+      const int pix = e >> 1, hh = e & 1;
+      const int sr = pix / kSC, sc = pix - (pix / kSC) * kSC;
+      const int y = sy0 + sr, x = sx0 + sc;
+      const bool ok = e < kSPieces && y < a.Hs && x < a.Ws;
+      roff[k] = ok ? (unsigned)((((long long)y * a.Ws + x) * a.in_cs + 4 * hh) * 4) : kWOOB;
+      roffm[k] = hh ? kWOOB : roff[k];
+      sdst[k] = e < kSPieces ? e : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < kXPer; ++k) {
+      const int e = tid + 256 * k;
+      const int pix = e >> 1, hh = e & 1;
+      const int rr = pix / kXRC, rc = pix - (pix / kXRC) * kXRC;
+      const int iy = 2 * ty0 - 1 + rr, ix = 2 * tx0 - 1 + rc;
+      int y0, y1, x0, x1;
+      float ly0, ly1, lx0, lx1;
+      krrn_src_index(max(iy, 0), a.Hs, a.sh, 1, y0, y1, ly0, ly1);
+      krrn_src_index(max(ix, 0), a.Ws, a.sw, 1, x0, x1, lx0, lx1);
+      const bool ok = e < kXPieces && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const int i00 = ((y0 - sy0) * kSC + (x0 - sx0)) * 2 + hh;
+      upk[k] = ok ? (i00 | ((y1 - y0) * kSC * 2) << 12 | ((x1 - x0) * 2) << 20) : -1;
+      uwy[k] = ly1;
+      uwx[k] = lx1;
+    }
+  }
+  f32x4 raw[kLPer];
   auto load_raw = [&](int ck) {  // chunks past the last reload the last (unused)
     ck = min(ck, nck - 1);
     const bool half = ck * kWC + 4 >= a.cin;
 #pragma unroll
-    for (int k = 0; k < kXPer; ++k)
+    for (int k = 0; k < kLPer; ++k)
       raw[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, half ? roffm[k] : roff[k],
                                                                               ck * kWC * 4, 0));
   };
-  auto store_raw = [&](int slot) {
-    f32x4* dst = reinterpret_cast<f32x4*>(smem) + slot * kXSlot;
+  f32x4* const sbuf = reinterpret_cast<f32x4*>(smem) + 3 * kXSlot;  // UP2 source buffers [2][kSPieces]
+  auto store_raw = [&](int slot) {  // !UP2: ring slot; UP2: source buffer
+    if constexpr (!UP2) {
+      f32x4* dst = reinterpret_cast<f32x4*>(smem) + slot * kXSlot;
 #pragma unroll
-    for (int k = 0; k < kXPer; ++k)
-      if (rdst[k] >= 0) dst[rdst[k]] = raw[k];
+      for (int k = 0; k < kXPer; ++k)
+        if (rdst[k] >= 0) dst[rdst[k]] = raw[k];
+    } else {
+      f32x4* dst = sbuf + slot * kSPieces;
+#pragma unroll
+      for (int k = 0; k < kSPer; ++k)
+        if (sdst[k] >= 0) dst[sdst[k]] = raw[k];
+    }
+  };
+  auto upsample = [&](int sslot, int rslot) {  // UP2: source buffer -> ring slot
+    const f32x4* src = sbuf + sslot * kSPieces;
+    f32x4* dst = reinterpret_cast<f32x4*>(smem) + rslot * kXSlot;
+#pragma unroll
+    for (int k = 0; k < kXPer; ++k) {
+      if (rdst[k] < 0) continue;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (upk[k] >= 0) {
+        const int i00 = upk[k] & 0xfff, dy = (upk[k] >> 12) & 0xff, dx = upk[k] >> 20;
+        v = krrn_bilerp4(src[i00], src[i00 + dx], src[i00 + dy], src[i00 + dy + dx], 1.f - uwy[k], uwy[k],
+                         1.f - uwx[k], uwx[k]);
+      }
+      dst[rdst[k]] = v;
+    }
   };
 
   // split weights (plane U_mh b128 + plane U_l b64 per (chunk, xi, n, half)), two buffers
@@ -691,20 +772,41 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       // keep the reload here (hipcc otherwise sinks every weight load below all the MFMAs)
       __builtin_amdgcn_sched_barrier(0);
     }
-    store_raw((ck + 2) % 3);
-    load_raw(ck + 3);
+    if constexpr (!UP2) {
+      store_raw((ck + 2) % 3);
+      load_raw(ck + 3);
+    } else {
+      upsample((ck + 2) & 1, (ck + 2) % 3);
+      store_raw((ck + 3) & 1);
+      load_raw(ck + 4);
+    }
     __syncthreads();
   };
 
   load_raw(0);
 #pragma unroll
   for (int v = 0; v < 4; ++v) load_wv(0, v);
-  store_raw(0);
-  load_raw(1);
-  __syncthreads();
-  store_raw(1);
-  load_raw(2);
-  __syncthreads();
+  if constexpr (!UP2) {
+    store_raw(0);
+    load_raw(1);
+    __syncthreads();
+    store_raw(1);
+    load_raw(2);
+    __syncthreads();
+  } else {
+    // source chunk c sits in buffer c & 1; up-sampled chunk c in ring slot c % 3
+    store_raw(0);
+    load_raw(1);
+    __syncthreads();
+    upsample(0, 0);
+    store_raw(1);
+    load_raw(2);
+    __syncthreads();
+    upsample(1, 1);
+    store_raw(0);
+    load_raw(3);
+    __syncthreads();
+  }
   for (int ck = 0; ck < nck; ++ck) chunk(ck);
 
   // epilogue: (c0, c1) = (M[u][0] + M[u][1] + M[u][2], M[u][1] - M[u][2] - M[u][3]) of every (tile,
@@ -849,11 +951,45 @@ KRRN_API int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int
   if (g_wino_x3_variant == 1) {
     const long long rbw = (long long)B * krrn_cdiv(a.Ht, kXGY) * krrn_cdiv(a.Wt, kXGX) * krrn_cdiv(N, kWN);
     if (rbw > 0x7fffffffLL) return KRRN_ESHAPE;
-    hipLaunchKernelGGL(wino_f23_x3w_kernel, dim3((unsigned)rbw), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(wino_f23_x3w_kernel<false>, dim3((unsigned)rbw), dim3(256), 0, (hipStream_t)stream, a);
     return krrn_launch_status();
   }
   const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kWN);
   if (rb > 0x7fffffffLL) return KRRN_ESHAPE;
   hipLaunchKernelGGL(wino_f23_x3_kernel, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_conv3x3_wino_x3_up2_f32(const float* in, int in_cs, int in_co, int B, int Hs, int Ws, int cin,
+                                          const void* U3, int N, int n_store, const float* scale, const float* bias,
+                                          const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
+                                          int relu, void* stream) {
+  if (!in || !U3 || !out) return KRRN_EARG;
+  if (B < 1 || Hs < 2 || Ws < 2 || N < 1 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
+  if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(U3) || !krrn_aligned16(in)) return KRRN_EALIGN;
+  if (out_co + n_store > out_cs) return KRRN_ESHAPE;
+  WinoArgs a;
+  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = 2 * Hs; a.W = 2 * Ws; a.cin = cin;
+  a.Hs = Hs; a.Ws = Ws;
+  a.sh = (float)(Hs - 1) / (float)(2 * Hs - 1);  // align_corners=True (krrn_resize_bilinear_f32's scale)
+  a.sw = (float)(Ws - 1) / (float)(2 * Ws - 1);
+  a.img = (long long)Hs * Ws * in_cs;
+  a.U = reinterpret_cast<const float*>(U3); a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
+  a.res = res; a.res_cs = res_cs; a.res_co = res_co;
+  a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.relu = relu;
+  a.Ht = Hs; a.Wt = Ws;
+  const bool ov = !(out_cs & 3) && !(out_co & 3) && krrn_aligned16(out);
+  const bool rv = !res || (!(res_cs & 3) && !(res_co & 3) && krrn_aligned16(res));
+  const bool sv = (!scale || krrn_aligned16(scale)) && (!bias || krrn_aligned16(bias));
+  a.vec = (ov && rv && sv && !(n_store & 3)) ? 1 : 0;
+  const long long T = (long long)B * a.Ht * a.Wt;
+  if (T > 0x7fffffffLL) return KRRN_ESHAPE;
+  a.T = (int)T;
+  const long long nrec = (long long)krrn_cdiv(cin, kWC) * 16 * N * 2;
+  if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
+  const long long rbw = (long long)B * krrn_cdiv(a.Ht, kXGY) * krrn_cdiv(a.Wt, kXGX) * krrn_cdiv(N, kWN);
+  if (rbw > 0x7fffffffLL) return KRRN_ESHAPE;
+  hipLaunchKernelGGL(wino_f23_x3w_kernel<true>, dim3((unsigned)rbw), dim3(256), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }

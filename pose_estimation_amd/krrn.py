@@ -92,9 +92,7 @@ class KRRNPlan:
         X = model.XYZNet
         h = bld.conv(xmap, X[0], X[1], relu=True)
         h = bld.conv(h, X[3], X[4], relu=True)
-        up = bld.act(2 * h.H, 2 * h.W, h.c)
-        bld.resize(h, up, align=True)
-        h = bld.conv(up, X[7], X[8], relu=True)
+        h = bld.conv_up2(h, X[7], X[8], relu=True)
         h = bld.conv(h, X[10], X[11], relu=True)
         self.xyz_outc = model.xyz_outc
         self.fx = plan.buf((B, model.xyz_outc, h.H, h.W))
@@ -106,9 +104,7 @@ class KRRNPlan:
         with plan.on_stream(1):
             g = bld.conv(ymap, Nn[0], Nn[1], relu=True)
             g = bld.conv(g, Nn[3], Nn[4], relu=True)
-            upn = bld.act(2 * g.H, 2 * g.W, g.c)
-            bld.resize(g, upn, align=True)
-            g = bld.conv(upn, Nn[7], Nn[8], relu=True)
+            g = bld.conv_up2(g, Nn[7], Nn[8], relu=True)
             self.fn = plan.buf((B, 3 * C, g.H, g.W))
             spec_n = ops.make_conv(model.nml_final, None, device, cin_p=g.cp)
             bld.specs.append(spec_n)
