@@ -78,6 +78,11 @@ typedef struct krrn_conv_desc {
   float* out;
   int out_cs, out_co, Ho, Wo, osy, osx, ooy, oox, relu, out_nchw, splits;
   float* workspace;
+  /* k order of wt: 0 = tap-major (k = tap*cin + c); Q > 0 (Q % 4 == 0, Q | cin) = channel-chunk
+   * major, k = ((c / Q)*ntaps + tap)*Q + c % Q: a block walks every tap of a Q-channel slice of
+   * its input pixels back to back, so the taps' overlapping reads hit L1 / L2 instead of re-fetching
+   * a whole tap's slab (the transposed convs' parity classes). Grouped launches only. */
+  int k_chunk;
 } krrn_conv_desc;
 
 /* Up to 4 independent convolutions in ONE launch with a shared tile shape (tile 1 = 128x128x16,

@@ -72,6 +72,10 @@ struct ConvArgs {
   // the epilogue (deterministic: no atomics).
   int kt_per;
   float* ws;
+  // channel-chunk-major k (krrn_conv_desc.k_chunk = Q > 0): k = ((c / Q) * ntaps + tap) * Q + c % Q
+  int kchunk;
+  unsigned kc_magic;  // ceil(2^32 / (Q * ntaps))
+  unsigned q_magic;   // ceil(2^32 / Q)
 };
 
 template <int BM, int BN, int BK, int WGM>
@@ -206,8 +210,17 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
 
   auto load_tile = [&](Stage<AL, BL, X3>& st) {
     // (tap, channel) of k without a divide or a data-dependent loop
-    const int tap = (int)__umulhi((unsigned)kk, a.cin_magic);
-    const int cc = kk - tap * a.cin;
+    int tap, cc;
+    if (a.kchunk) {
+      const int ch = (int)__umulhi((unsigned)kk, a.kc_magic);
+      const int rem = kk - ch * a.kchunk * a.ntaps;
+      tap = (int)__umulhi((unsigned)rem, a.q_magic);
+      cc = ch * a.kchunk + rem - tap * a.kchunk;
+      if (kk >= a.K) tap = 31;  // K tail: no tap, reads 0
+    } else {
+      tap = (int)__umulhi((unsigned)kk, a.cin_magic);
+      cc = kk - tap * a.cin;
+    }
     const unsigned toff = (unsigned)(stap[min(tap, 15)] + cc);
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
@@ -571,6 +584,15 @@ int prepare(const krrn_conv_desc& d, int& tile, ConvArgs& a, int& splits, bool x
   a.img = (long long)Hi * Wi * d.in_cs;
   a.cin_magic = (unsigned)((0x100000000ULL + cin - 1) / cin);
   if ((long long)(a.K + 64) * cin >= 0x100000000LL) return KRRN_ESHAPE;
+  a.kchunk = d.k_chunk;
+  a.kc_magic = a.q_magic = 0;
+  if (d.k_chunk) {
+    const int Q = d.k_chunk;
+    if (Q < 0 || (Q & 3) || cin % Q) return KRRN_EALIGN;
+    a.kc_magic = (unsigned)((0x100000000ULL + Q * ntaps - 1) / (Q * ntaps));
+    a.q_magic = (unsigned)((0x100000000ULL + Q - 1) / Q);
+    if ((long long)(a.K + 64) * Q * ntaps >= 0x100000000LL) return KRRN_ESHAPE;
+  }
   // 32-bit buffer offsets: the images one tile can touch (<= 256 rows) and the weights
   const long long HWg = (long long)Hg * Wg;
   const long long span = ((256 + HWg - 1) / HWg + 1) * a.img * 4;
@@ -606,7 +628,7 @@ int conv2d(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin
   d.bias2 = bias2; d.b2_div = b2_div;
   d.res = res; d.res_cs = res_cs; d.res_co = res_co; d.out = out; d.out_cs = out_cs; d.out_co = out_co;
   d.Ho = Ho; d.Wo = Wo; d.osy = osy; d.osx = osx; d.ooy = ooy; d.oox = oox; d.relu = relu;
-  d.out_nchw = out_nchw; d.splits = splits; d.workspace = workspace;
+  d.out_nchw = out_nchw; d.splits = splits; d.workspace = workspace; d.k_chunk = 0;
   ConvArgs a;
   int sp = 1;
   const int st = prepare(d, tile, a, sp, x3);

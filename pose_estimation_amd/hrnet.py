@@ -39,6 +39,9 @@ DECONV_FOLD = os.environ.get("KRRN_DECONV_FOLD", "1") == "1"
 # transposed convs (4 parity-class convs) as one grouped launch
 CONVT_GROUP = os.environ.get("KRRN_CONVT_GROUP", "1") == "1"
 CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
+# k order of the grouped transposed convs: channel chunks of this many channels outer, taps inner
+# (krrn_conv_desc.k_chunk; 0 = tap-major)
+CONVT_KCHUNK = int(os.environ.get("KRRN_CONVT_KCHUNK", "0"))
 # narrow 3x3 stride-1 convs (the HRNet branches' BasicBlocks) on the LDS-staged direct kernel
 SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
 # wide 1x1 convs as hipBLASLt GEMMs
@@ -336,9 +339,17 @@ class _Builder:
                           oox=oox, relu=relu, cin=spec.cin, cout=spec.cout)
                      for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off))]
             x3 = CONV_X3
+            q = CONVT_KCHUNK if CONVT_KCHUNK and spec.cin_p % CONVT_KCHUNK == 0 else 0
+            wts = [ops.kchunk_weights(w, len(t), spec.cin_p, q) for w, t in zip(spec.wt, spec.taps)] if q else spec.wt
+            for pr in probs:
+                pr["k_chunk"] = q
+            if q and not x3:
+                for pr, w in zip(probs, wts):
+                    self.specs.append(w)
+                    pr["wt"] = ptr(w)
             if x3:
                 for pr, cls in zip(probs, range(len(probs))):
-                    w3 = ops.conv_weights_x3(spec.wt[cls])
+                    w3 = ops.conv_weights_x3(wts[cls])
                     self.specs.append(w3)
                     pr["wt"] = ptr(w3)
             # split-bf16: the 128x128x16 tile (profiles/bench_conv_x3.py: transposed 4x4 272 -> 128 at

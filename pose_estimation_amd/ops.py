@@ -273,6 +273,13 @@ def conv_weights_x3(wt: torch.Tensor) -> torch.Tensor:
     return torch.cat([m, h, l, torch.zeros_like(l)], dim=-1).contiguous()
 
 
+def kchunk_weights(wt: torch.Tensor, ntaps: int, cin: int, q: int) -> torch.Tensor:
+    """Conv weights [N][ntaps * cin] (k = tap * cin + c) -> the channel-chunk-major order of
+    krrn_conv_desc.k_chunk = q: k = ((c / q) * ntaps + tap) * q + c % q."""
+    N = wt.shape[0]
+    return wt.reshape(N, ntaps, cin // q, q).permute(0, 2, 1, 3).reshape(N, ntaps * cin).contiguous()
+
+
 def gemm_weights_x3(wt: torch.Tensor) -> torch.Tensor:
     """GEMM weights [N][K] f32 (scale folded) -> the wave fragments krrn_gemm_x3_f32 reads: int32
     [N/32][K/8][2][64][4]. Fragment (column block nb, 8-k group g, quad q) is one coalesced 1-KB

@@ -69,7 +69,8 @@ class ConvDesc(ctypes.Structure):
                 ("Wg", I), ("in_s", I), ("ntaps", I), ("tap_dy", I * 9), ("tap_dx", I * 9), ("wt", P), ("N", I),
                 ("n_store", I), ("scale", P), ("bias", P), ("bias2", P), ("b2_div", I), ("res", P), ("res_cs", I),
                 ("res_co", I), ("out", P), ("out_cs", I), ("out_co", I), ("Ho", I), ("Wo", I), ("osy", I),
-                ("osx", I), ("ooy", I), ("oox", I), ("relu", I), ("out_nchw", I), ("splits", I), ("workspace", P)]
+                ("osx", I), ("ooy", I), ("oox", I), ("relu", I), ("out_nchw", I), ("splits", I), ("workspace", P),
+                ("k_chunk", I)]
 
 STREAM = "__stream__"
 
@@ -376,7 +377,7 @@ def add_small_group(plan: Plan, problems: List[dict], tag: str = "small_group"):
 
 def conv_desc(*, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_store, scale, bias, res=None,
               res_cs=0, res_co=0, out, out_cs, out_co, Ho, Wo, osy=1, osx=1, ooy=0, oox=0, relu=False,
-              splits=1, ws=None) -> ConvDesc:
+              splits=1, ws=None, k_chunk=0) -> ConvDesc:
     d = ConvDesc()
     d.in_, d.in_cs, d.in_co, d.B, d.Hi, d.Wi, d.cin, d.Hg, d.Wg, d.in_s = x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s
     d.ntaps = len(taps)
@@ -388,6 +389,7 @@ def conv_desc(*, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_s
     d.out, d.out_cs, d.out_co, d.Ho, d.Wo = out, out_cs, out_co, Ho, Wo
     d.osy, d.osx, d.ooy, d.oox, d.relu, d.out_nchw = osy, osx, ooy, oox, int(relu), 0
     d.splits, d.workspace = splits, (ws if ws is not None else P(0))
+    d.k_chunk = k_chunk
     return d
 
 

@@ -223,6 +223,46 @@ def test_conv_group_matches_single(dev, tile, x3):
         assert torch.equal(out.t, ref.t)
 
 
+@pytest.mark.parametrize("cin,k,op,x3,q", [(272, 4, 0, True, 16), (128, 3, 1, True, 16), (272, 4, 0, False, 16),
+                                           (128, 3, 1, True, 32), (40, 4, 0, True, 8)])
+def test_convT_group_kchunk(dev, cin, k, op, x3, q):
+    """The grouped transposed conv with channel-chunk-major k (krrn_conv_desc.k_chunk = q, weights
+    through ops.kchunk_weights) vs torch fp32 and vs the tap-major launch (same products, another
+    summation order: within f32 accumulation noise)."""
+    from pose_estimation_amd.runtime import add_conv_group, Plan, ptr
+    g = torch.Generator().manual_seed(cin + k + q)
+    B, H, cout = 3, 13, 128
+    convT = nn.ConvTranspose2d(cin, cout, k, 2, 1, output_padding=op, bias=False)
+    with torch.no_grad():
+        convT.weight.copy_(0.05 * torch.randn(convT.weight.shape, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, H, generator=g)
+    ref = torch.relu(bn(convT(x))).detach()
+    spec = ops.make_convT(convT, bn, dev)
+    xa = _nhwc(x, dev)
+    Ho, Wo = ref.shape[2:]
+    got = []
+    for kc in (0, q):
+        out = ops.new_act(B, Ho, Wo, cout, dev)
+        out.t.fill_(float("nan"))
+        plan = Plan(dev)
+        probs, keep = [], []
+        for w, taps, (ooy, oox) in zip(spec.wt, spec.taps, spec.cls_off):
+            w = ops.kchunk_weights(w, len(taps), spec.cin_p, kc) if kc else w
+            w = ops.conv_weights_x3(w) if x3 else w
+            keep.append(w)
+            probs.append(dict(x=ptr(xa.t), x_cs=xa.cs, x_co=0, B=B, Hi=H, Wi=H, cin_p=spec.cin_p, Hg=H, Wg=H, in_s=1,
+                              taps=taps, wt=ptr(w), N=cout, n_store=cout, scale=ptr(spec.scale), bias=ptr(spec.bias),
+                              out=ptr(out.t), out_cs=out.cs, out_co=0, Ho=Ho, Wo=Wo, osy=2, osx=2, ooy=ooy, oox=oox,
+                              relu=True, cin=cin, cout=cout, k_chunk=kc))
+        add_conv_group(plan, probs, tile=1 if x3 else 8, x3=x3)
+        plan.run({})
+        torch.cuda.synchronize()
+        got.append(out.t[..., :cout].permute(0, 3, 1, 2).cpu())
+    torch.testing.assert_close(got[1], ref, **TOL)
+    torch.testing.assert_close(got[1], got[0], rtol=1e-5, atol=2e-6 * float(ref.abs().max()))
+
+
 @pytest.mark.parametrize("cin,cout,H,W,co", [(128, 128, 30, 30, 0), (64, 72, 17, 23, 4), (272, 272, 15, 15, 0),
                                              (36, 40, 9, 8, 8), (20, 132, 61, 35, 0), (128, 64, 120, 120, 0)])
 def test_conv3x3_winograd(dev, cin, cout, H, W, co):
