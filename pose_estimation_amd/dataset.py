@@ -44,7 +44,7 @@ import torch
 
 from . import _lib
 from .config import CONFIG, LM_OBJLIST, OBJ_DICT, SYM_OBJ, models_info
-from .runtime import P, ptr
+from .runtime import P, h2d, ptr
 from .synthetic import LM_K, rand_rotation
 
 _I = ctypes.c_int
@@ -184,8 +184,8 @@ def build_inputs(frames: Dict[str, torch.Tensor], frame_idx: Sequence[int], boxe
     if len(sizes) != 1:
         raise ValueError(f"one crop size per batch (bucket by get_square_bbox first), got {sorted(sizes)}")
     S = sizes.pop()
-    fi = torch.tensor(list(frame_idx), dtype=torch.int32).to(dev)
-    rc = torch.tensor([[b[0], b[2]] for b in boxes], dtype=torch.int32).to(dev)
+    fi = h2d(torch.tensor(list(frame_idx), dtype=torch.int32), dev)
+    rc = h2d(torch.tensor([[b[0], b[2]] for b in boxes], dtype=torch.int32), dev)
     img = torch.empty((B, 3, S, S), dtype=torch.float32, device=dev)
     mask = torch.empty((B, S * S), dtype=torch.uint8, device=dev)
     st = P(torch.cuda.current_stream(dev).cuda_stream)
@@ -197,7 +197,7 @@ def build_inputs(frames: Dict[str, torch.Tensor], frame_idx: Sequence[int], boxe
     xm = torch.empty((B, N, 1), dtype=torch.float32, device=dev)
     ym = torch.empty((B, N, 1), dtype=torch.float32, device=dev)
     cnt = torch.empty((B,), dtype=torch.int32, device=dev)
-    K4 = K4.to(device=dev, dtype=torch.float32).contiguous()
+    K4 = h2d(K4, dev, torch.float32)
     _lib.call("krrn_choose_points", ptr(mask), B, S, N, ptr(depth), H, W, ptr(fi), ptr(rc), ptr(K4), float(depth_scale),
               ptr(seed), int(stream_id), ptr(choose), ptr(cloud), ptr(xm), ptr(ym), ptr(cnt), st)
     return {"img_croped": img, "choose": choose, "cloud": cloud, "x_map_choosed": xm, "y_map_choosed": ym,
@@ -342,9 +342,9 @@ class PoseDataset(torch.utils.data.Dataset):
         """Decode the batch's frames from the tree (thread pool) and stage them on `device`."""
         with ThreadPoolExecutor(max_workers=max(1, min(self.io_threads, len(idx)))) as ex:
             fr = list(ex.map(self.tree.read, idx))
-        return {"rgb": torch.from_numpy(np.stack([f[0] for f in fr])).to(device, non_blocking=True),
-                "depth": torch.from_numpy(np.stack([f[1] for f in fr])).to(device, non_blocking=True),
-                "mask_label": torch.from_numpy(np.stack([f[2] for f in fr])).to(device, non_blocking=True)}
+        return {"rgb": h2d(torch.from_numpy(np.stack([f[0] for f in fr])), device),
+                "depth": h2d(torch.from_numpy(np.stack([f[1] for f in fr])), device),
+                "mask_label": h2d(torch.from_numpy(np.stack([f[2] for f in fr])), device)}
 
     def _meta(self, i: int):
         """(obj id, R [3,3] f64, t [3] f64, model points [P,3] f32) of crop i."""
@@ -390,7 +390,7 @@ class PoseDataset(torch.utils.data.Dataset):
             # model_points @ target_r.T + target_t in f64, then float32 (batchdataset.py:706, 765)
             "target": (mp.double() @ R64.transpose(1, 2) + t64[:, None]).float(),
         }
-        out.update({k: v.to(device) for k, v in host.items()})
+        out.update({k: h2d(v, device) for k, v in host.items()})
         return out
 
     def __getitem__(self, i: int) -> Dict[str, torch.Tensor]:

@@ -42,7 +42,7 @@ from .fusion import FEAT_SID, FusionNetLite, build_fusion_plan, level_sizes
 from .hrnet import _Builder, build_hrnet, build_hrnet_plan
 from .ops import Act, pad4
 from .posenet import PoseNet, build_tbase_plan, emit_tbase_level1
-from .runtime import Late, Plan, add_conv, ptr
+from .runtime import Late, Plan, add_conv, h2d, ptr
 
 # the wide head's final 1x1 conv (xyz_final, K = 128) on split-bf16 operands (f32 accuracy,
 # krrn_conv1x1_nchw_x3_f32) instead of f32 MFMAs
@@ -240,7 +240,7 @@ class KRRNPlan:
         elif mode == "host":
             # torch.randperm(vertice_num)[:pool_num] on the CPU generator, in module call order
             for k, n, m in self.perm_sizes:
-                self.perms[k].copy_(torch.randperm(n)[:m].to(torch.int32), non_blocking=True)
+                self.perms[k].copy_(h2d(torch.randperm(n)[:m].to(torch.int32), self.perms[k].device), non_blocking=True)
         elif mode == "device":
             self.device_perm_plan.run({})
         else:

@@ -16,7 +16,7 @@ import torch
 import ctypes
 
 from . import _lib
-from .runtime import P, ptr
+from .runtime import P, h2d, ptr
 
 _I = ctypes.c_int
 _lib.register("krrn_add_metric_f32", [P, P, P, P, P, P, _I, _I, _I, P, P, P])
@@ -30,12 +30,12 @@ def add_metric(pred_r: torch.Tensor, pred_t: torch.Tensor, model_points: torch.T
     if dev.type != "cuda":
         raise RuntimeError("add_metric runs on the HIP path only (GPU tensors)")
     B, Pn = model_points.shape[0], model_points.shape[1]
-    f = lambda x: x.to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
-    symt = torch.tensor(list(sym) or [0], dtype=torch.int32, device=dev)
+    f = lambda x: h2d(x, dev, torch.float32)  # noqa: E731
+    symt = h2d(torch.tensor(list(sym) or [0], dtype=torch.int32), dev)
     ws = torch.empty((B * ((Pn + 255) // 256),), dtype=torch.float64, device=dev)
     out = torch.empty((B,), dtype=torch.float64, device=dev)
     _lib.call("krrn_add_metric_f32", ptr(f(pred_r).reshape(B, 9)), ptr(f(pred_t).reshape(B, 3)), ptr(f(model_points)),
-              ptr(f(target)), ptr(cls_id.to(device=dev, dtype=torch.int64).reshape(B).contiguous()), ptr(symt),
+              ptr(f(target)), ptr(h2d(cls_id.reshape(B), dev, torch.int64)), ptr(symt),
               len(sym), B, Pn, ptr(ws), ptr(out), P(torch.cuda.current_stream(dev).cuda_stream))
     return out
 

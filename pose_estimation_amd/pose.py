@@ -18,7 +18,7 @@ from typing import Dict, Optional
 
 import torch
 
-from .runtime import P, Plan, ptr
+from .runtime import P, Plan, h2d, ptr
 from . import _lib
 
 NUM_POINTS = 256
@@ -37,8 +37,7 @@ def _seed(device) -> torch.Tensor:
 
 
 def _dev(t: torch.Tensor, device, dtype=None) -> torch.Tensor:
-    t = t.to(device=device, dtype=dtype if dtype is not None else t.dtype, non_blocking=True)
-    return t.contiguous()
+    return h2d(t, device, dtype)
 
 
 def draw_sel(B: int, N: int, num_points: int = NUM_POINTS) -> torch.Tensor:

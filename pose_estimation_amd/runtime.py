@@ -83,6 +83,20 @@ def ptr(t: Optional[torch.Tensor]) -> P:
     return P(t.data_ptr()) if t is not None else P(0)
 
 
+def h2d(t: torch.Tensor, device, dtype=None) -> torch.Tensor:
+    """`t` on `device` (as `dtype`), contiguous. A host tensor bound for the GPU goes through pinned
+    memory with a non-blocking copy: a copy from pageable memory is synchronous on this runtime, so it
+    would stall the host until the stream drained and serialise the next batch's host-side preparation
+    behind the GPU work already queued (the eval epoch's per-batch inputs, perms and metric operands).
+    torch's pinned allocator keeps the staging block alive until the copy has run."""
+    device = torch.device(device)
+    if dtype is not None and t.dtype != dtype and t.device.type == "cpu":
+        t = t.to(dtype)
+    if t.device.type == "cpu" and device.type == "cuda":
+        t = t.contiguous().pin_memory()
+    return t.to(device=device, dtype=dtype if dtype is not None else t.dtype, non_blocking=True).contiguous()
+
+
 class Late:
     """A late-bound argument: the pointer of env[key] (or env[key] itself if not a tensor)."""
     __slots__ = ("key",)
