@@ -11,7 +11,10 @@ half-step:
   shadow != serial                 -> the surface conv itself produced wrong values (or a store
                                       landed between it and the copy).
 It also reports the wrong entries' values against zero and against the other slot's F0 (the two
-slots load different batches here, so a value read across slots is recognisable).
+slots load different batches here, so a value read across slots is recognisable). Before every
+graph half-step both slots' F0 and shadows are filled with sentinels (-7 / -9): F0 is recomputed
+from the same inputs each rep, so a lost store or a read of a stale copy would otherwise show the
+previous rep's identical value; with the sentinel, a store that never reached memory reads -7.
 
 usage (GPU box): KRRN_STREAMS=1 python3 profiles/f0_shadow.py [REPS] [--history]"""
 import os
@@ -92,6 +95,10 @@ for rep in range(REPS):
     for sl, s in zip(pp.slots, s0):
         sl.parts[0].kp.seed.copy_(s)
     pp.reset()
+    for f, sh in zip(F0s, shadows):
+        f.fill_(-7.0)
+        sh.fill_(-9.0)
+    torch.cuda.synchronize()
     pp.step()  # B(0) beside A(1)
     torch.cuda.synchronize()
     f0g, shg, f01 = F0s[0].clone(), shadows[0].clone(), F0s[1].clone()
@@ -119,5 +126,10 @@ for rep in range(REPS):
         wrong = f0g[d_f0]
         if wrong.numel():
             print(f"   wrong F0 values: zero {int((wrong == 0).sum())} of {wrong.numel()}; equal to slot-1 F0 "
-                  f"{int((f0g[d_f0] == f01[d_f0]).sum())}", flush=True)
+                  f"{int((f0g[d_f0] == f01[d_f0]).sum())}; sentinel (store lost) {int((wrong == -7.0).sum())}",
+                  flush=True)
+        wsh = shg[d_sh]
+        if wsh.numel():
+            print(f"   wrong shadow values: sentinel (copy lost) {int((wsh == -9.0).sum())}, F0 sentinel read "
+                  f"{int((wsh == -7.0).sum())} of {wsh.numel()}", flush=True)
 print(f"{bad_reps} of {REPS} half-steps mismatched", flush=True)
