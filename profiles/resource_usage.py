@@ -1,0 +1,80 @@
+"""Per-kernel register / scratch / LDS / occupancy table of libkrrn_hip.so's sources, from hipcc's
+`-Rpass-analysis=kernel-resource-usage` remarks with the Makefile's flags (per-file FLAGS_* included).
+CPU only (hipcc cross-compiles for gfx950):
+
+    python3 profiles/resource_usage.py [--out profiles/r4_resource_usage.txt]
+
+Every kernel with ScratchSize > 0 is flagged: a spill in a hot loop costs HBM traffic per launch
+(VERDICT r3 weak #6 / #7)."""
+import argparse
+import os
+import re
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "pose_estimation_amd", "csrc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast-honor-pragmas"]
+EXTRA = {"pnp": ["-ffp-contract=off"], "winograd": ["-fno-slp-vectorize"]}
+FIELDS = ("VGPRs", "AGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "LDS Size [bytes/block]", "TotalSGPRs",
+          "VGPRs Spill")
+
+
+def demangle(names):
+    try:
+        out = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True,
+                             text=True, check=True).stdout.split("\n")
+        return [o.replace("(anonymous namespace)::", "") for o in out[:len(names)]]
+    except (OSError, subprocess.CalledProcessError):
+        return names
+
+
+def kernels(src):
+    stem = os.path.splitext(os.path.basename(src))[0]
+    with tempfile.TemporaryDirectory() as td:
+        r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *EXTRA.get(stem, []), "-c", src, "-o",
+                            os.path.join(td, "k.o"), "-Rpass-analysis=kernel-resource-usage"],
+                           capture_output=True, text=True)
+    rows, cur = [], None
+    for line in r.stderr.split("\n"):
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = {"name": m.group(1), "file": stem}
+            rows.append(cur)
+            continue
+        m = re.search(r"remark:\s+([A-Za-z][^:]*?): (\d+)", line)
+        if m and cur is not None and m.group(1) in FIELDS:
+            cur[m.group(1)] = int(m.group(2))
+    names = demangle([r["name"] for r in rows])
+    for r, n in zip(rows, names):
+        r["name"] = n.split("(")[0]
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    rows = []
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith(".hip"):
+            rows += kernels(os.path.join(CSRC, f))
+    hdr = f"{'file':14s} {'VGPR':>4s} {'AGPR':>4s} {'SGPR':>4s} {'scratch':>7s} {'spill':>5s} {'occ':>3s} {'LDS':>6s}  kernel"
+    lines = [hdr]
+    for r in rows:
+        lines.append(f"{r['file']:14s} {r.get('VGPRs', 0):4d} {r.get('AGPRs', 0):4d} {r.get('TotalSGPRs', 0):4d} "
+                     f"{r.get('ScratchSize [bytes/lane]', 0):7d} {r.get('VGPRs Spill', 0):5d} {r.get('Occupancy [waves/SIMD]', 0):3d} "
+                     f"{r.get('LDS Size [bytes/block]', 0):6d}  {r['name']}")
+    spills = [r for r in rows if r.get("ScratchSize [bytes/lane]", 0) > 0]
+    lines.append("")
+    lines.append(f"{len(rows)} kernels; scratch > 0: " + (", ".join(f"{r['name']} ({r['ScratchSize [bytes/lane]']} B)"
+                                                              for r in spills) or "none"))
+    text = "\n".join(lines)
+    print(text)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(text + "\n")
+
+
+if __name__ == "__main__":
+    main()
