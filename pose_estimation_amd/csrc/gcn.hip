@@ -17,6 +17,8 @@
 
 #include "krrn_common.h"
 
+#include <mutex>
+
 namespace {
 
 constexpr int kKnnThreads = 256;
@@ -359,7 +361,8 @@ template <bool HAS_Y, int KC, bool BUF = true>
 __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     const int* __restrict__ idx, int n, const float* __restrict__ v, long long v_bs, int v_st,
     const float* __restrict__ dn, int S, const float* __restrict__ Y, const float* __restrict__ bn_s,
-    const float* __restrict__ bn_b, int relu, float* __restrict__ out, long long o_bs, int o_st) {
+    const float* __restrict__ bn_b, int relu, float* __restrict__ out, long long o_bs, int o_st,
+    unsigned* __restrict__ dbg) {
   constexpr int C = 128, LP = 32, kPts = kGcnThreads / LP;
   __shared__ f32x4 sdn[3 * kGcnSmax * C / 4];
   __shared__ float sdir[kPts * KC * 3];
@@ -387,6 +390,16 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     const float nr = fmaxf(sqrtf(ss), 1e-12f);
 #pragma unroll
     for (int i = 0; i < 3; ++i) sdir[(p * KC + j) * 3 + i] = dv[i] / nr;
+    if (!HAS_Y && dbg) {  // diagnostics (krrn_gcn_debug): the neighbour and coordinates as read
+      unsigned* r = dbg + (((long long)b * n + pi) * KC + j) * 8;
+      r[0] = (unsigned)nj;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        r[1 + i] = __float_as_uint(vb[(long long)pi * v_st + i]);
+        r[4 + i] = __float_as_uint(vb[(long long)nj * v_st + i]);
+      }
+      r[7] = (unsigned)b;
+    }
   }
   __syncthreads();
   const int p = threadIdx.x / LP, l = threadIdx.x % LP;
@@ -458,6 +471,29 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
 
 }  // namespace
 
+namespace {
+// krrn_gcn_debug: where the surface convs (Y == NULL) of the 3-D form dump, per (crop, point,
+// neighbour), the neighbour index and both points' coordinates as the kernel read them (8 words).
+// Launch i writes slot i % nslots. Diagnostics only (profiles/f0_shadow.py); off unless set.
+struct GcnDebug {
+  std::mutex mu;
+  unsigned* buf = nullptr;
+  long long slot_words = 0;
+  int nslots = 1;
+  long long count = 0;
+} g_gcn_dbg;
+}  // namespace
+
+KRRN_API int krrn_gcn_debug(void* buf, int nslots, long long slot_words) {
+  const std::lock_guard<std::mutex> lk(g_gcn_dbg.mu);
+  if (buf && (nslots < 1 || slot_words < 1)) return KRRN_EARG;
+  g_gcn_dbg.buf = reinterpret_cast<unsigned*>(buf);
+  g_gcn_dbg.nslots = nslots < 1 ? 1 : nslots;
+  g_gcn_dbg.slot_words = slot_words;
+  g_gcn_dbg.count = 0;
+  return KRRN_OK;
+}
+
 KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, long long v_bs, int v_st, int d,
                                const float* dn, int S, int C, const float* Y, const float* bn_scale,
                                const float* bn_bias, int relu, float* out, long long o_bs, int o_st, int B,
@@ -485,9 +521,14 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   const bool use3 = legacy == 0 || (legacy == 2 && !Y) || (legacy == 3 && Y);
   if (use3 && d == 3 && C == 128 && S <= kGcnSmax && (k == 10 || k == 8) &&
       (long long)n * (S + 1) * C * 4 < (1LL << 31)) {
+    unsigned* dbg = nullptr;
+    if (!Y && g_gcn_dbg.buf) {
+      const std::lock_guard<std::mutex> lk(g_gcn_dbg.mu);
+      dbg = g_gcn_dbg.buf + (g_gcn_dbg.count++ % g_gcn_dbg.nslots) * g_gcn_dbg.slot_words;
+    }
 #define KRRN_GCN3(HY, KC, BF) \
   hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC, BF>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
-                     bn_scale, bn_bias, relu, out, o_bs, o_st)
+                     bn_scale, bn_bias, relu, out, o_bs, o_st, dbg)
     if (Y) {
       if (bufload) {
         if (k == 10) KRRN_GCN3(true, 10, true); else KRRN_GCN3(true, 8, true);

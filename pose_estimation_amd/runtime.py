@@ -29,6 +29,7 @@ U = ctypes.c_uint
 # C-ABI signatures (include/krrn_hip.h); every function returns int status.
 _lib.register("krrn_knn_f32", [P, L, I, I, P, P, L, I, I, I, I, I, I, I, P, P])
 _lib.register("krrn_gcn_conv_f32", [P, I, I, P, L, I, I, P, I, I, P, P, P, I, P, L, I, I, P])
+_lib.register("krrn_gcn_debug", [P, I, L])
 _lib.register("krrn_pool_max_f32", [P, I, I, P, L, I, I, P, L, I, I, P])
 _lib.register("krrn_resize_bilinear_f32", [P, I, I, I, I, I, I, P, I, I, I, I, P, I, I, I, I, P])
 _lib.register("krrn_add_relu_f32", [P, I, I, P, I, I, P, I, I, L, I, I, P])

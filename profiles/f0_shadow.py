@@ -26,7 +26,7 @@ import torch  # noqa: E402
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-from pose_estimation_amd import KRRN, make_config  # noqa: E402
+from pose_estimation_amd import KRRN, _lib, make_config  # noqa: E402
 from pose_estimation_amd.pipeline import PipelinedPipeline, _sub_plan  # noqa: E402
 from pose_estimation_amd.runtime import Late, Op, P, ptr, _skey  # noqa: E402
 from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
@@ -88,7 +88,18 @@ for si, sl in enumerate(pp.slots):
 s0 = [sl.parts[0].kp.seed.clone() for sl in pp.slots]
 pp.run()
 torch.cuda.synchronize()
+# surface-conv input dumps (krrn_gcn_debug): per (crop, point, neighbour) the neighbour index and the
+# coordinates the kernel read. capture() runs B(0), A(0), B(1), A(1) eagerly, then captures them in
+# that order: launches 0-5 and again 6-11 -> slots 0-2 = slot 0's v / x / n branches, 3-5 = slot 1's
+K0 = 10
+WORDS = B * N * K0 * 8
+dump_g = torch.zeros(6 * WORDS, dtype=torch.int32, device=dev)
+dump_s = torch.zeros(3 * WORDS, dtype=torch.int32, device=dev)
+_lib.call("krrn_gcn_debug", ptr(dump_g), 6, WORDS)
 pp.capture()
+_lib.call("krrn_gcn_debug", P(0), 1, 1)
+kp0 = pp.slots[0].parts[0].kp
+P9, IDX0 = kp0.p9, kp0.fusion_bufs["idx0"]
 F0s = [sl.parts[0].kp.fusion_bufs["F0"] for sl in pp.slots]
 bad_reps = 0
 for rep in range(REPS):
@@ -102,10 +113,30 @@ for rep in range(REPS):
     pp.step()  # B(0) beside A(1)
     torch.cuda.synchronize()
     f0g, shg, f01 = F0s[0].clone(), shadows[0].clone(), F0s[1].clone()
+    p9g, idxg, dg = P9.clone(), IDX0.clone(), dump_g[:3 * WORDS].clone()
     pp.slots[0].parts[0].kp.seed.copy_(s0[0])
+    _lib.call("krrn_gcn_debug", ptr(dump_s), 3, WORDS)
     pp._run_b(0)  # serial re-run of slot 0's stage B from the same state
     torch.cuda.synchronize()
+    _lib.call("krrn_gcn_debug", P(0), 1, 1)
     f0s = F0s[0].clone()
+    print(f"   after the graph step vs the serial re-run: p9 differs at {int((p9g != P9).sum())}, idx0 at "
+          f"{int((idxg != IDX0).sum())} entries", flush=True)
+    for br in range(3):
+        g_ = dg[br * WORDS:(br + 1) * WORDS].view(B, N, K0, 8)
+        s_ = dump_s[br * WORDS:(br + 1) * WORDS].view(B, N, K0, 8)
+        d_nb = g_[..., 0] != s_[..., 0]
+        d_pi = (g_[..., 1:4] != s_[..., 1:4]).any(-1)
+        d_nj = (g_[..., 4:7] != s_[..., 4:7]).any(-1)
+        print(f"   branch {br} as read by the surface conv (graph vs serial): neighbour index differs at "
+              f"{int(d_nb.sum())}, point coords at {int(d_pi.sum())}, neighbour coords at {int(d_nj.sum())} of "
+              f"{d_nb.numel()} (crop, point, j)", flush=True)
+        bad = (d_nb | d_pi | d_nj).nonzero()[:6].tolist()
+        for b_, p_, j_ in bad:
+            gr, sr = g_[b_, p_, j_].tolist(), s_[b_, p_, j_].tolist()
+            f = lambda w: [round(float(torch.tensor(w, dtype=torch.int32).view(torch.float32)), 7) for w in w]  # noqa: E731
+            print(f"     [{b_},{p_},{j_}] graph nb {gr[0]} p {f(gr[1:4])} nb {f(gr[4:7])} | serial nb {sr[0]} "
+                  f"p {f(sr[1:4])} nb {f(sr[4:7])}", flush=True)
     d_f0 = (f0g != f0s)
     d_sh = (shg != f0s)
     print(f"rep {rep}: F0(graph) != F0(serial) at {int(d_f0.sum())} entries / {int(d_f0.any(-1).sum())} points; "

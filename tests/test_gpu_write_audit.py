@@ -42,9 +42,12 @@ def _audit_pipeline(dev, B, S, N):
             for pi, (plan, env) in enumerate(lists[si]):
                 runs.append((f"{stage}{si}.{pi}", plan, env))
     extra = [(f"slot{si}", sl.parts[0]) for si, sl in enumerate(pp.slots)]
-    rep = audit(runs, extra=extra, names=_names(pp))
+    owners = [sl.parts[0].kp.plan for sl in pp.slots]  # the stage views own no buffers
+    names = _names(pp)
+    rep = audit(runs, extra=extra, names=names, owners=owners)
+    rep["n_names"] = len(names)
     print(f"audit B={B} S={S} N={N}: {rep['ops']} calls, {rep['regions']} buffers "
-          f"({rep['bytes'] / 1e9:.2f} GB) watched; {rep['n_violations']} stray writes, "
+          f"({rep['bytes'] / 1e9:.2f} GB, {rep['named']} named) watched; {rep['n_violations']} stray writes, "
           f"{rep['n_input_changes']} const-input writes")
     for v in rep["violations"] + rep["input_changes"]:
         print("  ", v)
@@ -66,12 +69,12 @@ def test_header_params_cover_plan_entry_points():
 def test_write_audit_small_after_history(dev):
     _history(dev)
     rep = _audit_pipeline(dev, 4, 64, 256)
-    assert rep["ops"] > 800
+    assert rep["ops"] > 800 and rep["named"] == rep["n_names"] and rep["regions"] > 100
     assert rep["n_violations"] == 0 and rep["n_input_changes"] == 0, rep
 
 
 @pytest.mark.gpu
 def test_write_audit_benched_shape(dev):
     rep = _audit_pipeline(dev, 64, 120, 1000)
-    assert rep["ops"] > 800
+    assert rep["ops"] > 800 and rep["named"] == rep["n_names"] and rep["regions"] > 100 and rep["bytes"] > 1e9
     assert rep["n_violations"] == 0 and rep["n_input_changes"] == 0, rep

@@ -186,21 +186,26 @@ def _host_desc_arrays(plans) -> Dict[int, Any]:
 
 
 def audit(runs: Sequence[Tuple[str, Any, dict]], extra: Sequence[Tuple[str, Any]] = (),
-          names: Optional[Dict[str, torch.Tensor]] = None, max_report: int = 20) -> Dict[str, Any]:
-    """runs: (label, Plan, env) in execution order. Every plan buffer of every plan (and the tensors
-    reachable from `extra`) is watched; `names` labels some of them in the report. Returns {'ops': n, 'regions': n, 'bytes': n,
-    'violations': [...], 'input_changes': [...], 'unwritten_ops': [...]}: a violation is
+          names: Optional[Dict[str, torch.Tensor]] = None, max_report: int = 20,
+          owners: Sequence[Any] = ()) -> Dict[str, Any]:
+    """runs: (label, Plan, env) in execution order. Every plan buffer of every plan and of `owners`
+    (the whole plans that sub-plan views in `runs` were cut from: a view owns no buffers) and the
+    tensors reachable from `extra` are watched; `names` labels some of them in the report. Returns
+    {'ops': n, 'regions': n, 'bytes': n, 'violations': [...], 'input_changes': [...]}: a violation is
     (label, op index, entry point, region label + shape, stream id)."""
     from pose_estimation_amd.runtime import Op
     params = header_pointer_params()
-    plans = [p for _, p, _ in runs]
-    objs = [(f"{lab}.buffers", p.buffers) for lab, p, _ in runs] + list(extra)
+    plans = [p for _, p, _ in runs] + list(owners)
+    objs = ([(f"{lab}.buffers", p.buffers) for lab, p, _ in runs] +
+            [(f"owner{i}.buffers", p.buffers) for i, p in enumerate(owners)] + list(extra))
     regs = plan_regions(objs)
     loc = _Locator(regs)
+    named = 0
     for nm, t in (names or {}).items():
         i = loc.find(t.data_ptr()) if isinstance(t, torch.Tensor) and t.is_cuda else None
         if i is not None:
             regs[i].label = nm
+            named += 1
     host = _host_desc_arrays(plans)
     dev = regs[0].t.device
     stream = torch.cuda.current_stream(dev)
@@ -225,6 +230,6 @@ def audit(runs: Sequence[Tuple[str, Any, dict]], extra: Sequence[Tuple[str, Any]
                 rec = (lab, oi, op.name, f"{regs[i].label}{tuple(regs[i].t.shape)}", op.sid,
                        "const input" if i in rd else "not an argument")
                 (inchg if i in rd else viol).append(rec)
-    return {"ops": nops, "regions": len(regs), "bytes": sum(r.hi - r.lo for r in regs),
+    return {"ops": nops, "regions": len(regs), "bytes": sum(r.hi - r.lo for r in regs), "named": named,
             "violations": viol[:max_report], "n_violations": len(viol),
             "input_changes": inchg[:max_report], "n_input_changes": len(inchg)}
