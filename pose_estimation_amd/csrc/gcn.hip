@@ -402,6 +402,36 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     }
   }
   __syncthreads();
+  if (!HAS_Y && dbg) {
+    // diagnostics: a per-block digest of the staged directions as this block's LDS holds them, and
+    // the XCD / CU the block ran on, after the per-point records ([B][n][KC][8] words)
+    __shared__ unsigned sdig[2];
+    if (threadIdx.x == 0) sdig[0] = sdig[1] = 0u;
+    __syncthreads();
+    unsigned x = 0u, a = 0u;
+    for (int e = threadIdx.x; e < 3 * SC / 4; e += kGcnThreads) {
+      const f32x4 q = sdn[e];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned u = __float_as_uint(q[i]);
+        x ^= u * (unsigned)(4 * e + i + 1);
+        a += u;
+      }
+    }
+    atomicXor(&sdig[0], x);
+    atomicAdd(&sdig[1], a);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned xcc, hwid;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+      unsigned* r = dbg + (long long)gridDim.y * n * KC * 8 + (long long)lin * 4;
+      r[0] = sdig[0];
+      r[1] = sdig[1];
+      r[2] = xcc;
+      r[3] = hwid;
+    }
+  }
   const int p = threadIdx.x / LP, l = threadIdx.x % LP;
   if (p >= np) return;
   const int pi = p0 + p;
