@@ -425,11 +425,21 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
       unsigned xcc, hwid;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-      unsigned* r = dbg + (long long)gridDim.y * n * KC * 8 + (long long)lin * 4;
+      unsigned* r = dbg + (long long)gridDim.y * n * KC * 8 + (long long)lin * 12;
       r[0] = sdig[0];
       r[1] = sdig[1];
       r[2] = xcc;
       r[3] = hwid;
+      // the kernel arguments as this block sees them
+      const unsigned long long po = (unsigned long long)out, pd = (unsigned long long)dn, pv = (unsigned long long)v;
+      r[4] = (unsigned)po;
+      r[5] = (unsigned)(po >> 32);
+      r[6] = (unsigned)o_bs;
+      r[7] = (unsigned)o_st;
+      r[8] = (unsigned)S;
+      r[9] = (unsigned)relu;
+      r[10] = (unsigned)pd;
+      r[11] = (unsigned)pv;
     }
   }
   const int p = threadIdx.x / LP, l = threadIdx.x % LP;

@@ -94,7 +94,7 @@ torch.cuda.synchronize()
 K0 = 10
 GX = -(-N // 8)  # blocks per crop of the surface conv (8 points per block)
 REC = B * N * K0 * 8
-WORDS = REC + 4 * B * GX
+WORDS = REC + 12 * B * GX
 if "--retouch" in sys.argv:
     # rewrite every plan-owned tensor through a device kernel (read + write back through the L2s)
     # before the captures: tells constants written by host-to-device copies from kernel-written ones
@@ -141,8 +141,11 @@ for rep in range(REPS):
     for br in range(3):
         g_ = dg[br * WORDS:br * WORDS + REC].view(B, N, K0, 8)
         s_ = dump_s[br * WORDS:br * WORDS + REC].view(B, N, K0, 8)
-        gb = dg[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 4)
-        sb = dump_s[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 4)
+        gb = dg[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 12)
+        sb = dump_s[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 12)
+        da_ = (gb[:, 4:] != sb[:, 4:]).any(-1)
+        print(f"   branch {br}: blocks whose kernel arguments differ from the serial run's: {int(da_.sum())}; "
+              f"distinct argument sets in the graph {len(set(map(tuple, gb[:, 4:].tolist())))}", flush=True)
         dd_ = (gb[:, :2] != sb[:, :2]).any(-1)
         wrong_pts = (f0g[..., 128 * br:128 * (br + 1)] != f0s[..., 128 * br:128 * (br + 1)]).any(-1)  # [B, N]
         wb = sorted({int(b_) * GX + int(p_) // 8 for b_, p_ in wrong_pts.nonzero().tolist()})
@@ -185,6 +188,17 @@ for rep in range(REPS):
                   f"shadow {float(shg[b, n, c]):+.6e} slot1 {float(f01[b, n, c]):+.6e}", flush=True)
         wrong = f0g[d_f0]
         if wrong.numel():
+            # where else do the wrong values occur in the serial F0 (another point / slice / crop)?
+            flat = f0s.flatten()
+            hits = 0
+            for k_, (b_, n_, c_) in enumerate(d_f0.nonzero().tolist()[:40]):
+                w_ = f0g[b_, n_, c_]
+                pos = (flat == w_).nonzero().flatten().tolist()
+                hits += bool(pos)
+                if k_ < 8:
+                    wh = [(q // (N * 384), (q // 384) % N, q % 384) for q in pos[:3]]
+                    print(f"     wrong [{b_},{n_},{c_}] = {float(w_):+.7e} found in serial F0 at {wh}", flush=True)
+            print(f"   {hits} of {min(40, wrong.numel())} wrong values occur somewhere in the serial F0", flush=True)
             print(f"   wrong F0 values: zero {int((wrong == 0).sum())} of {wrong.numel()}; equal to slot-1 F0 "
                   f"{int((f0g[d_f0] == f01[d_f0]).sum())}; sentinel (store lost) {int((wrong == -7.0).sum())}",
                   flush=True)
