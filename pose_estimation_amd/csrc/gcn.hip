@@ -357,7 +357,9 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
 //     carries no 64-bit address arithmetic (the old form kept ten 64-bit pointers and stepped
 //     them every support: 228 VGPRs, 2 waves per SIMD);
 //   * __launch_bounds__(256, 4): >= 4 waves per SIMD, each with its k gather loads in flight.
-template <bool HAS_Y, int KC, bool BUF = true>
+// DBG (diagnostics, krrn_gcn_debug; surface convs only): per-point / per-block records of what the
+// block read and held in LDS, at the start and at the end of the support loop.
+template <bool HAS_Y, int KC, bool BUF = true, bool DBG = false>
 __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     const int* __restrict__ idx, int n, const float* __restrict__ v, long long v_bs, int v_st,
     const float* __restrict__ dn, int S, const float* __restrict__ Y, const float* __restrict__ bn_s,
@@ -390,7 +392,7 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     const float nr = fmaxf(sqrtf(ss), 1e-12f);
 #pragma unroll
     for (int i = 0; i < 3; ++i) sdir[(p * KC + j) * 3 + i] = dv[i] / nr;
-    if (!HAS_Y && dbg) {  // diagnostics (krrn_gcn_debug): the neighbour and coordinates as read
+    if constexpr (!HAS_Y && DBG) {  // the neighbour and coordinates as read
       unsigned* r = dbg + (((long long)b * n + pi) * KC + j) * 8;
       r[0] = (unsigned)nj;
 #pragma unroll
@@ -402,13 +404,12 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     }
   }
   __syncthreads();
-  if (!HAS_Y && dbg) {
-    // diagnostics: a per-block digest of the staged directions as this block's LDS holds them, and
-    // the XCD / CU the block ran on, after the per-point records ([B][n][KC][8] words)
-    __shared__ unsigned sdig[2];
-    if (threadIdx.x == 0) sdig[0] = sdig[1] = 0u;
+  __shared__ unsigned sdig[4];
+  // digest of the staged directions (sdn) and point directions (sdir) as this block's LDS holds them
+  auto digest = [&](unsigned* r) {
+    if (threadIdx.x == 0) sdig[0] = sdig[1] = sdig[2] = sdig[3] = 0u;
     __syncthreads();
-    unsigned x = 0u, a = 0u;
+    unsigned x = 0u, a = 0u, x2 = 0u, a2 = 0u;
     for (int e = threadIdx.x; e < 3 * SC / 4; e += kGcnThreads) {
       const f32x4 q = sdn[e];
 #pragma unroll
@@ -418,32 +419,51 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
         a += u;
       }
     }
+    for (int e = threadIdx.x; e < np * KC * 3; e += kGcnThreads) {
+      const unsigned u = __float_as_uint(sdir[e]);
+      x2 ^= u * (unsigned)(e + 1);
+      a2 += u;
+    }
     atomicXor(&sdig[0], x);
     atomicAdd(&sdig[1], a);
+    atomicXor(&sdig[2], x2);
+    atomicAdd(&sdig[3], a2);
     __syncthreads();
+    if (threadIdx.x == 0) {
+      r[0] = sdig[0];
+      r[1] = sdig[1];
+      r[2] = sdig[2];
+      r[3] = sdig[3];
+    }
+  };
+  unsigned* rblk = nullptr;
+  if constexpr (!HAS_Y && DBG) {
+    // per block (after the per-point records): digests at the start (0-3), XCC / HW id (4, 5), the
+    // kernel arguments as read (6-13), digests after the support loop (16-19)
+    rblk = dbg + (long long)gridDim.y * n * KC * 8 + (long long)lin * 20;
+    digest(rblk);
     if (threadIdx.x == 0) {
       unsigned xcc, hwid;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-      unsigned* r = dbg + (long long)gridDim.y * n * KC * 8 + (long long)lin * 12;
-      r[0] = sdig[0];
-      r[1] = sdig[1];
-      r[2] = xcc;
-      r[3] = hwid;
-      // the kernel arguments as this block sees them
       const unsigned long long po = (unsigned long long)out, pd = (unsigned long long)dn, pv = (unsigned long long)v;
-      r[4] = (unsigned)po;
-      r[5] = (unsigned)(po >> 32);
-      r[6] = (unsigned)o_bs;
-      r[7] = (unsigned)o_st;
-      r[8] = (unsigned)S;
-      r[9] = (unsigned)relu;
-      r[10] = (unsigned)pd;
-      r[11] = (unsigned)pv;
+      rblk[4] = xcc;
+      rblk[5] = hwid;
+      rblk[6] = (unsigned)po;
+      rblk[7] = (unsigned)(po >> 32);
+      rblk[8] = (unsigned)o_bs;
+      rblk[9] = (unsigned)o_st;
+      rblk[10] = (unsigned)S;
+      rblk[11] = (unsigned)relu;
+      rblk[12] = (unsigned)pd;
+      rblk[13] = (unsigned)pv;
     }
   }
   const int p = threadIdx.x / LP, l = threadIdx.x % LP;
-  if (p >= np) return;
+  if constexpr (!(!HAS_Y && DBG)) {
+    if (p >= np) return;
+  }
+  const bool live = p < np;
   const int pi = p0 + p;
   const int c = 4 * l;
   const int yrow = (S + 1) * C;
@@ -506,7 +526,11 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     if (bn_s) o[q] = o[q] * bn_s[c + q] + bn_b[c + q];
     if (relu) o[q] = fmaxf(o[q], 0.f);
   }
-  *reinterpret_cast<f32x4*>(out + b * o_bs + (long long)pi * o_st + c) = o;
+  if (live) *reinterpret_cast<f32x4*>(out + b * o_bs + (long long)pi * o_st + c) = o;
+  if constexpr (!HAS_Y && DBG) {
+    __syncthreads();
+    digest(rblk + 16);
+  }
 }
 
 }  // namespace
@@ -569,6 +593,15 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
 #define KRRN_GCN3(HY, KC, BF) \
   hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC, BF>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
                      bn_scale, bn_bias, relu, out, o_bs, o_st, dbg)
+    if (dbg) {
+      if (k == 10)
+        hipLaunchKernelGGL((gcn_conv3_kernel<false, 10, true, true>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs,
+                           v_st, dn, S, Y, bn_scale, bn_bias, relu, out, o_bs, o_st, dbg);
+      else
+        hipLaunchKernelGGL((gcn_conv3_kernel<false, 8, true, true>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs,
+                           v_st, dn, S, Y, bn_scale, bn_bias, relu, out, o_bs, o_st, dbg);
+      return krrn_launch_status();
+    }
     if (Y) {
       if (bufload) {
         if (k == 10) KRRN_GCN3(true, 10, true); else KRRN_GCN3(true, 8, true);

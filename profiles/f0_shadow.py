@@ -94,7 +94,7 @@ torch.cuda.synchronize()
 K0 = 10
 GX = -(-N // 8)  # blocks per crop of the surface conv (8 points per block)
 REC = B * N * K0 * 8
-WORDS = REC + 12 * B * GX
+WORDS = REC + 20 * B * GX
 if "--retouch" in sys.argv:
     # rewrite every plan-owned tensor through a device kernel (read + write back through the L2s)
     # before the captures: tells constants written by host-to-device copies from kernel-written ones
@@ -141,21 +141,28 @@ for rep in range(REPS):
     for br in range(3):
         g_ = dg[br * WORDS:br * WORDS + REC].view(B, N, K0, 8)
         s_ = dump_s[br * WORDS:br * WORDS + REC].view(B, N, K0, 8)
-        gb = dg[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 12)
-        sb = dump_s[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 12)
-        da_ = (gb[:, 4:] != sb[:, 4:]).any(-1)
+        gb = dg[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 20)
+        sb = dump_s[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 20)
+        da_ = (gb[:, 6:14] != sb[:, 6:14]).any(-1)
         print(f"   branch {br}: blocks whose kernel arguments differ from the serial run's: {int(da_.sum())}; "
-              f"distinct argument sets in the graph {len(set(map(tuple, gb[:, 4:].tolist())))}", flush=True)
+              f"distinct argument sets in the graph {len(set(map(tuple, gb[:, 6:14].tolist())))}", flush=True)
+        de_g = (gb[:, 16:20] != gb[:, 0:4]).any(-1)
+        de_s = (sb[:, 16:20] != sb[:, 0:4]).any(-1)
+        print(f"   branch {br}: blocks whose LDS changed during the support loop: graph {int(de_g.sum())}, serial "
+              f"{int(de_s.sum())}; point-direction digest differs graph vs serial before the loop in "
+              f"{int((gb[:, 2:4] != sb[:, 2:4]).any(-1).sum())} blocks", flush=True)
         dd_ = (gb[:, :2] != sb[:, :2]).any(-1)
         wrong_pts = (f0g[..., 128 * br:128 * (br + 1)] != f0s[..., 128 * br:128 * (br + 1)]).any(-1)  # [B, N]
         wb = sorted({int(b_) * GX + int(p_) // 8 for b_, p_ in wrong_pts.nonzero().tolist()})
-        xg = (gb[:, 2] & 0xF).tolist()
+        xg = (gb[:, 4] & 0xF).tolist()
         print(f"   branch {br}: blocks whose staged-direction digest differs from the serial run: {int(dd_.sum())} "
               f"of {B * GX} (XCDs {sorted(set(xg[i] for i in dd_.nonzero().flatten().tolist()))}); distinct graph "
               f"digests {len(set(map(tuple, gb[:, :2].tolist())))}, serial {len(set(map(tuple, sb[:, :2].tolist())))}; "
               f"blocks holding wrong F0 points {len(wb)}, their XCDs {sorted(set(xg[i] for i in wb))}, digest differs in "
               f"{sum(int(dd_[i]) for i in wb)}", flush=True)
-        for i in wb[:4]:
+        print(f"   branch {br}: of the blocks holding wrong points, LDS changed during the loop in "
+              f"{sum(int(de_g[i]) for i in wb)}", flush=True)
+        for i in wb[:3]:
             print(f"     block {i}: graph {gb[i].tolist()} serial {sb[i].tolist()}", flush=True)
         d_nb = g_[..., 0] != s_[..., 0]
         d_pi = (g_[..., 1:4] != s_[..., 1:4]).any(-1)
