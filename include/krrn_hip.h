@@ -267,8 +267,10 @@ int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, long long v_
  * XCD remap) 20 words: digests of the staged directions and of the point directions as the block's
  * LDS holds them before the support loop (4), the XCC id and HW_ID register it ran on (2), the
  * arguments out (2 words), o_bs, o_st, S, relu, dn, v (low words) as the block read them (8), two
- * unused, the same digests after the support loop (4). Launch i goes into slot i % nslots of `buf`
- * (slot_words u32 each, >= B * n * k * 8 + 20 * B * ceil(n / 8)). buf = NULL turns it off; every call resets the launch
+ * unused, the same digests after the support loop (4); then per (block, thread, support s < 8)
+ * 8 floats: the support's max and the first direction-weight quad as held in registers. Launch i
+ * goes into slot i % nslots of `buf` (slot_words u32 each, >= B * n * k * 8 + 20 * nb + 16384 * nb
+ * with nb = B * ceil(n / 8) blocks). buf = NULL turns it off; every call resets the launch
  * count. Not for production runs (one host mutex per surface-conv launch). */
 int krrn_gcn_debug(void* buf, int nslots, long long slot_words);
 

@@ -517,6 +517,14 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], 0.f);
     }
+    if constexpr (!HAS_Y && DBG) {
+      // per (block, thread, support): the support's max and the first direction-weight quad as
+      // this thread held them in registers (after the per-block records)
+      float* rt = reinterpret_cast<float*>(dbg + (long long)gridDim.y * n * KC * 8 + (long long)gridDim.x * gridDim.y * 20) +
+                  (((long long)lin * kGcnThreads + threadIdx.x) * kGcnSmax + s) * 8;
+      *reinterpret_cast<f32x4*>(rt) = m;
+      *reinterpret_cast<f32x4*>(rt + 4) = w[0];
+    }
     acc += m;
   }
   f32x4 o = acc;

@@ -94,7 +94,8 @@ torch.cuda.synchronize()
 K0 = 10
 GX = -(-N // 8)  # blocks per crop of the surface conv (8 points per block)
 REC = B * N * K0 * 8
-WORDS = REC + 20 * B * GX
+NBLK = B * GX
+WORDS = REC + 20 * NBLK + 16384 * NBLK
 if "--retouch" in sys.argv:
     # rewrite every plan-owned tensor through a device kernel (read + write back through the L2s)
     # before the captures: tells constants written by host-to-device copies from kernel-written ones
@@ -141,8 +142,10 @@ for rep in range(REPS):
     for br in range(3):
         g_ = dg[br * WORDS:br * WORDS + REC].view(B, N, K0, 8)
         s_ = dump_s[br * WORDS:br * WORDS + REC].view(B, N, K0, 8)
-        gb = dg[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 20)
-        sb = dump_s[br * WORDS + REC:(br + 1) * WORDS].view(B * GX, 20)
+        gb = dg[br * WORDS + REC:br * WORDS + REC + 20 * NBLK].view(NBLK, 20)
+        sb = dump_s[br * WORDS + REC:br * WORDS + REC + 20 * NBLK].view(NBLK, 20)
+        gt = dg[br * WORDS + REC + 20 * NBLK:(br + 1) * WORDS].view(torch.float32).view(NBLK, 256, 8, 8)
+        st_ = dump_s[br * WORDS + REC + 20 * NBLK:(br + 1) * WORDS].view(torch.float32).view(NBLK, 256, 8, 8)
         da_ = (gb[:, 6:14] != sb[:, 6:14]).any(-1)
         print(f"   branch {br}: blocks whose kernel arguments differ from the serial run's: {int(da_.sum())}; "
               f"distinct argument sets in the graph {len(set(map(tuple, gb[:, 6:14].tolist())))}", flush=True)
@@ -162,6 +165,17 @@ for rep in range(REPS):
               f"{sum(int(dd_[i]) for i in wb)}", flush=True)
         print(f"   branch {br}: of the blocks holding wrong points, LDS changed during the loop in "
               f"{sum(int(de_g[i]) for i in wb)}", flush=True)
+        # per (thread, support): the support max and the first weight quad as held in registers
+        Sn = 7
+        dm = (gt[:, :, :Sn, 0:4] != st_[:, :, :Sn, 0:4]).any(-1)   # [NBLK, 256, S]
+        dw = (gt[:, :, :Sn, 4:8] != st_[:, :, :Sn, 4:8]).any(-1)
+        print(f"   branch {br}: (thread, support) records whose max differs {int(dm.sum())}, whose weight quad "
+              f"differs {int(dw.sum())}; both {int((dm & dw).sum())}", flush=True)
+        for blk, th_, s_ in dm.nonzero()[:6].tolist():
+            w_prev = st_[blk, th_, s_ - 1, 4:8].tolist() if s_ > 0 else None
+            print(f"     blk {blk} thr {th_} s {s_}: max g {gt[blk, th_, s_, 0:4].tolist()} s {st_[blk, th_, s_, 0:4].tolist()}"
+                  f" | w g {gt[blk, th_, s_, 4:8].tolist()} s {st_[blk, th_, s_, 4:8].tolist()} (serial w at s-1 {w_prev})",
+                  flush=True)
         for i in wb[:3]:
             print(f"     block {i}: graph {gb[i].tolist()} serial {sb[i].tolist()}", flush=True)
         d_nb = g_[..., 0] != s_[..., 0]
