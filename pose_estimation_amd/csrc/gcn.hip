@@ -219,10 +219,6 @@ KRRN_API int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, cons
 namespace {
 
 constexpr int kGcnThreads = 256;
-// scalar f32 VALU only (no v_pk_mul_f32 / v_pk_fma_f32): see DESIGN.md section 5 (the round-4
-// cross-kernel mismatch of the surface conv); the results are bit-identical either way
-#pragma clang diagnostic ignored "-Wignored-attributes"
-#define KRRN_NO_PK_F32 __attribute__((target("no-packed-fp32-ops")))
 constexpr int kGcnKmax = 16;
 constexpr int kGcnSmax = 8;  // support_num bound of the LDS-staged 3-D form (the model uses 7)
 #ifndef GCN3_WAVES
@@ -364,7 +360,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
 // DBG (diagnostics, krrn_gcn_debug; surface convs only): per-point / per-block records of what the
 // block read and held in LDS, at the start and at the end of the support loop.
 template <bool HAS_Y, int KC, bool BUF = true, bool DBG = false>
-__global__ __launch_bounds__(256, GCN3_WAVES) KRRN_NO_PK_F32 void gcn_conv3_kernel(
+__global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     const int* __restrict__ idx, int n, const float* __restrict__ v, long long v_bs, int v_st,
     const float* __restrict__ dn, int S, const float* __restrict__ Y, const float* __restrict__ bn_s,
     const float* __restrict__ bn_b, int relu, float* __restrict__ out, long long o_bs, int o_st,

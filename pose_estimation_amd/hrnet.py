@@ -41,7 +41,7 @@ CONVT_GROUP = os.environ.get("KRRN_CONVT_GROUP", "1") == "1"
 CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
 # k order of the grouped transposed convs: channel chunks of this many channels outer, taps inner
 # (krrn_conv_desc.k_chunk; 0 = tap-major)
-CONVT_KCHUNK = int(os.environ.get("KRRN_CONVT_KCHUNK", "0"))
+CONVT_KCHUNK = int(os.environ.get("KRRN_CONVT_KCHUNK", "16"))
 # narrow 3x3 stride-1 convs (the HRNet branches' BasicBlocks) on the LDS-staged direct kernel
 SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
 # wide 1x1 convs as hipBLASLt GEMMs
@@ -52,7 +52,7 @@ FUSE_ID_FIRST = os.environ.get("KRRN_FUSE_ID_FIRST", "1") == "1"
 WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
 # the heads' x2 upsample + 3x3 conv as one launch (krrn_conv3x3_wino_x3_up2_f32: the upsample is
 # blended while the Winograd input is staged, never written)
-UP2_FUSE = os.environ.get("KRRN_UP2_FUSE", "0") == "1"
+UP2_FUSE = os.environ.get("KRRN_UP2_FUSE", "1") == "1"
 # implicit-GEMM convs (transposed convs, stem / transitions) likewise (krrn_conv2d[_group]_x3_f32)
 CONV_X3 = os.environ.get("KRRN_CONV_X3", "1") == "1"
 

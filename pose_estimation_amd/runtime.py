@@ -152,10 +152,13 @@ class Sync:
 # were free); the outputs are meaningless with it set, and nothing in the package sets it.
 _DIAG_DROP = frozenset(filter(None, os.environ.get("KRRN_DIAG_DROP", "").split(",")))
 # KRRN_PLAN_STREAMS=1 (default): a plan captured into a hipGraph keeps its side streams (graph
-# branches); 0 = captured serially. KRRN_STREAMS=1: the two-slot pipeline's stages and concurrent
-# micro-batches replay side by side on two streams; default 0 = one after the other (Plan)
+# branches); 0 = captured serially. KRRN_STREAMS=1 (default): the two-slot pipeline's stages and
+# concurrent micro-batches replay side by side on two streams; 0 = one after the other. Rounds 3-4
+# kept it off while two graphs side by side gave a different level-0 surface-conv output; the cause
+# was a packed-FP32 VALU result going wrong beside the split-bf16 Winograd, and the library is now
+# built without packed-FP32 ops
 PLAN_STREAMS = os.environ.get("KRRN_PLAN_STREAMS", "1") == "1"
-STREAMS = os.environ.get("KRRN_STREAMS", "0") == "1"
+STREAMS = os.environ.get("KRRN_STREAMS", "1") == "1"
 
 
 class Plan:
@@ -168,12 +171,11 @@ class Plan:
 
     `run()` is serial by default (everything on the caller's stream); the side streams are used
     only with `run(serial=False)` under hipGraph capture, where every fork / join becomes a graph
-    edge (KRRN_PLAN_STREAMS=0 makes captured plans serial too). Eagerly, the plan's ~7 streams share
-    the GPU_MAX_HW_QUEUES = 4 hardware queues and a kernel intermittently read an input its producer
-    on another stream had not finished (round 2). One captured plan graph at a time has matched the
-    serial run in every check; two graphs replayed on two streams at once (the
-    two-slot pipeline, concurrent micro-batches) did not, so those overlap only with KRRN_STREAMS=1
-    (pipeline.py)."""
+    edge (KRRN_PLAN_STREAMS=0 makes captured plans serial too). The mismatches that led to this
+    (round 2: eager plans on ~7 streams; round 3: two graphs side by side) were a packed-FP32 VALU
+    result going wrong while the split-bf16 Winograd ran on the same CU, not a missing dependency
+    (serial write audit clean, the kernel's inputs, LDS and arguments identical); the
+    library is built without packed-FP32 ops since round 4."""
 
     def __init__(self, device: torch.device):
         self.device = device

@@ -14,7 +14,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "pose_estimation_amd", "csrc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast-honor-pragmas"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast-honor-pragmas",
+         "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]  # as pose_estimation_amd/csrc/Makefile
 EXTRA = {"pnp": ["-ffp-contract=off"], "winograd": ["-fno-slp-vectorize"]}
 FIELDS = ("VGPRs", "AGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "LDS Size [bytes/block]", "TotalSGPRs",
           "VGPRs Spill")

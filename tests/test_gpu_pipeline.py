@@ -194,8 +194,8 @@ def test_pipelined_graph_benched_shape(dev):
 
 
 def test_benched_step_graph_after_history(dev):
-    """bench.py's step as benched (config 2: one hipGraph of the whole path, every launch on one
-    stream, runtime.STREAMS off) after the allocation history above: graph replays alternating
+    """bench.py's step as benched (config 2: one hipGraph of the whole path, the plan's branches as
+    graph branches) after the allocation history above: graph replays alternating
     between two RNG states each equal the eager serial step of that state bit for bit (a replay that
     read a buffer before this step wrote it would see the other state's values)."""
     _history(dev)
