@@ -248,7 +248,8 @@ __global__ __launch_bounds__(64 * kX3Waves) __attribute__((amdgpu_waves_per_eu(4
         for (int i = 0; i < 4; ++i) {
           const int n = 16 * t + 4 * g + i;
           if (n < n_store)
-            __builtin_amdgcn_raw_buffer_store_b32(acc[t][i] * ssc[n] + sbi[n], rso, vo, (16 * t + i) * HW * 4, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[t][i] * ssc[n] + sbi[n]), rso, vo,
+                                                  (16 * t + i) * HW * 4, 0);  // the f32 bits (b32 takes a u32)
         }
     }
   }
