@@ -51,8 +51,10 @@ FUSE_ID_FIRST = os.environ.get("KRRN_FUSE_ID_FIRST", "1") == "1"
 # Winograd convs on the bf16 matrix cores with f32-accurate split operands (krrn_conv3x3_wino_x3_f32)
 WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
 # the heads' x2 upsample + 3x3 conv as one launch (krrn_conv3x3_wino_x3_up2_f32: the upsample is
-# blended while the Winograd input is staged, never written)
-UP2_FUSE = os.environ.get("KRRN_UP2_FUSE", "1") == "1"
+# blended while the Winograd input is staged, never written). Off by default: the blend adds ~13 % of
+# VALU to an issue-bound kernel, about what the resize's 472 MB write + re-read costs (step medians
+# 5427 vs 5499 crops/s, three alternating runs on one box)
+UP2_FUSE = os.environ.get("KRRN_UP2_FUSE", "0") == "1"
 # implicit-GEMM convs (transposed convs, stem / transitions) likewise (krrn_conv2d[_group]_x3_f32)
 CONV_X3 = os.environ.get("KRRN_CONV_X3", "1") == "1"
 
