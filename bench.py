@@ -5,8 +5,8 @@ HRNet-W18 + heads + class select/normalise + choose gather + FusionNetLite + TBa
 + batched PnP-RANSAC (R), including the device-side randomness (pool permutations, the 256-
 point PnP subset, RANSAC hypotheses). The step is one hipGraph replay of the whole path (the plan's
 independent branches as graph branches, runtime.Plan); the two-slot pipeline (--pipeline
-heads|backbone|pose) and concurrent micro-batches overlap only with KRRN_STREAMS=1, which is not
-reproducible on this stack and measured no faster. With --gpus N
+heads|backbone|pose) and concurrent micro-batches replay side by side on two streams (KRRN_STREAMS=1,
+the default since the round-4 root cause) and measured no faster. With --gpus N
 (torchrun, one process per GPU, RCCL) every rank runs its own batch (weak scaling) and the
 per-crop pose records are all-gathered over RCCL after every step.
 
@@ -327,10 +327,33 @@ def bench_config3(args, rank: int, world: int, local: int):
             pl.capture()
             pipes.append(pl)
         record = torch.zeros((_config3_cap(buckets_all, world), kd.RECORD), dtype=torch.float32, device=dev)
+        # the buckets' graphs side by side on a few streams (most buckets hold 1-87 crops, each alone
+        # far too small to fill the chip): longest-processing-time assignment by crops x S^2
+        nst = max(1, min(args.c3_streams if STREAMS else 1, len(pipes)))
+        streams = [torch.cuda.Stream(dev) for _ in range(nst)] if nst > 1 else []
+        load = [0.0] * nst
+        assign = [0] * len(pipes)
+        for i in sorted(range(len(pipes)), key=lambda i: -pipes[i].B * pipes[i].S ** 2):
+            j = min(range(nst), key=lambda j: load[j])
+            assign[i] = j
+            load[j] += pipes[i].B * pipes[i].S ** 2
+
+        def run_buckets():
+            if not streams:
+                for pl in pipes:
+                    pl.step()
+                return
+            main = torch.cuda.current_stream(dev)
+            for s_ in streams:
+                s_.wait_stream(main)
+            for pl, j in zip(pipes, assign):
+                with torch.cuda.stream(streams[j]):
+                    pl.step()
+            for s_ in streams:
+                main.wait_stream(s_)
 
         def one_step():
-            for pl in pipes:
-                pl.step()
+            run_buckets()
             if world > 1:
                 o = 0
                 for pl in pipes:
@@ -444,10 +467,12 @@ def main():
                          "LineMOD test-crop histogram, bucketed by S and every bucket split across the ranks "
                          "(distributed.bucket_shard; strong scaling: the 256 crops are shared by the N GPUs)")
     ap.add_argument("--global-batch", type=int, default=256, help="config 3: crops per step over all ranks")
+    ap.add_argument("--c3-streams", type=int, default=3,
+                    help="config 3: streams the per-bucket graphs replay on side by side (1 = one after another)")
     ap.add_argument("--pipeline", choices=["none", "backbone", "heads", "pose"], default="none",
                     help="none (default): one batch per step end to end as one hipGraph; backbone / heads / pose: "
-                         "the two-stage pipeline (pipeline.PipelinedPipeline) split there, whose stages overlap only "
-                         "with KRRN_STREAMS=1 (not reproducible on this stack, DESIGN.md §5; measured no faster)")
+                         "the two-stage pipeline (pipeline.PipelinedPipeline) split there, its stages side by side on two "
+                         "streams (KRRN_STREAMS=1; measured no faster than one graph)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
