@@ -198,7 +198,14 @@ KRRN_API int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N
     // form that had room for it was removed: DESIGN.md §5)
     return KRRN_EUNSUPPORTED;
   }
-  if (K == 128) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 0>), grid, dim3(512), 0, s, g);
+  // KRRN_PANEL_DIAG (timing experiments only, outputs wrong): 1 = no MFMAs, 2 = no output stores
+  static const int diag = [] {
+    const char* e = getenv("KRRN_PANEL_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  if (K == 128 && diag == 1) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 1>), grid, dim3(512), 0, s, g);
+  else if (K == 128 && diag == 2) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 2>), grid, dim3(512), 0, s, g);
+  else if (K == 128) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 0>), grid, dim3(512), 0, s, g);
   else if (res) hipLaunchKernelGGL((gemm_plds_x3_kernel<64, true, 0>), grid, dim3(512), 0, s, g);
   else hipLaunchKernelGGL((gemm_plds_x3_kernel<64, false, 0>), grid, dim3(512), 0, s, g);
   return krrn_launch_status();
