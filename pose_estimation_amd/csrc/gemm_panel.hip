@@ -49,19 +49,30 @@ __device__ __forceinline__ gp_bf16x8 gp_op(const gp_u32x4 v) { return __builtin_
 
 // (The round-3 register-only form without the LDS ring re-streamed 768 KB of weight fragments per
 // wave from L2, 3 GB per level-0 launch, and was removed in round 4.)
-template <int KT, bool RES, int DIAG = 0>  // DIAG (measurements only): 1 = no MFMAs, 2 = no output stores
+typedef unsigned gp_u32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ gp_bf16x8 gp_sub4(const gp_u32x8& c, int o) {
+  return __builtin_bit_cast(gp_bf16x8, gp_u32x4{c[o], c[o + 1], c[o + 2], c[o + 3]});
+}
+
+// CH (chain layout, KRRN_PANEL_CHAIN): per 8-k group the weights are one [m h] quad + one [l] pair
+// per lane (ops.gemm_weights_panel_chain: 24 B instead of the three quads' 48 B), the activations a
+// register chain [h h m l]; the MFMAs take register slices, W[2:5] x A[0:3] = hh + lh,
+// W[0:3] x A[2:5] = mh + hm, W[0:3] x A[4:7] = mm + hl -- half the LDS bytes per MFMA.
+template <int KT, bool RES, int DIAG = 0, bool CH = false>  // DIAG (measurements only): 1 = no MFMAs, 2 = no stores
 __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g) {
   constexpr int G = KT / 8;
-  constexpr int TILE_U32 = G * 3 * 256;  // one 32-column tile of split fragments
-  constexpr int PIECES = TILE_U32 / 4 / 512;
-  static_assert(PIECES * 4 * 512 == TILE_U32, "tile staging");
+  constexpr int GU32 = CH ? 384 : 768;   // u32 per 8-k group of one 32-column tile
+  constexpr int TILE_U32 = G * GU32;     // one 32-column tile of split fragments
+  constexpr int P4 = TILE_U32 / 4;       // 16-B pieces per tile
+  constexpr int PIECES = (P4 + 511) / 512;
   __shared__ __attribute__((aligned(16))) unsigned sb[2][TILE_U32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nl = lane & 31, fh = lane >> 5;
   const int m0 = blockIdx.x * 256 + wave * 32;
 
   // ---- the wave's activation panel (rows past M are zero; every wave stays for the barriers) ----
-  gp_u32x4 qa[G][2];
+  gp_u32x4 qa[CH ? 1 : G][2];
+  gp_u32x8 ca[CH ? G : 1];
   {
     const int row = m0 + nl;
     const float* ap = g.a + (size_t)row * g.lda + 4 * fh;
@@ -78,8 +89,12 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
       const unsigned mm0 = gp_pk(r0, r1), mm1 = gp_pk(r2, r3);
       const unsigned l0 = gp_pk(r0 - __builtin_bit_cast(float, mm0 << 16), r1 - __builtin_bit_cast(float, mm0 & 0xFFFF0000u));
       const unsigned l1 = gp_pk(r2 - __builtin_bit_cast(float, mm1 << 16), r3 - __builtin_bit_cast(float, mm1 & 0xFFFF0000u));
-      qa[gi][0] = gp_u32x4{h0, h1, mm0, mm1};
-      qa[gi][1] = gp_u32x4{h0, h1, l0, l1};
+      if constexpr (CH) {
+        ca[gi] = gp_u32x8{h0, h1, h0, h1, mm0, mm1, l0, l1};
+      } else {
+        qa[gi][0] = gp_u32x4{h0, h1, mm0, mm1};
+        qa[gi][1] = gp_u32x4{h0, h1, l0, l1};
+      }
     }
   }
 
@@ -89,12 +104,14 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
   auto load_tile = [&](int ct) {
     const gp_u32x4* src = reinterpret_cast<const gp_u32x4*>(g.w + (size_t)ct * TILE_U32);
 #pragma unroll
-    for (int i = 0; i < PIECES; ++i) stg[i] = src[tid + i * 512];
+    for (int i = 0; i < PIECES; ++i)
+      if (P4 % 512 == 0 || tid + i * 512 < P4) stg[i] = src[tid + i * 512];
   };
   auto store_tile = [&](int buf) {
     gp_u32x4* dst = reinterpret_cast<gp_u32x4*>(sb[buf]);
 #pragma unroll
-    for (int i = 0; i < PIECES; ++i) dst[tid + i * 512] = stg[i];
+    for (int i = 0; i < PIECES; ++i)
+      if (P4 % 512 == 0 || tid + i * 512 < P4) dst[tid + i * 512] = stg[i];
   };
   if (ct0 < ct1) {
     load_tile(ct0);
@@ -152,12 +169,21 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       if (live && has && DIAG != 1) {
-        const gp_u32x4 b0 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768);
-        const gp_u32x4 b1 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768 + 256);
-        const gp_u32x4 b2 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768 + 512);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(b0), gp_op(qa[gi][0]), acc, 0, 0, 0);  // mm + hh
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(b1), gp_op(qa[gi][0]), acc, 0, 0, 0);  // mh + hm
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(b2), gp_op(qa[gi][1]), acc, 0, 0, 0);  // lh + hl
+        if constexpr (CH) {
+          const gp_u32x4 mh = *reinterpret_cast<const gp_u32x4*>(bp + gi * 384);
+          const unsigned* lp = sb[buf] + gi * 384 + 256 + lane * 2;
+          const gp_u32x8 wc = {mh[0], mh[1], mh[2], mh[3], lp[0], lp[1], 0u, 0u};  // [m h l]
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_sub4(wc, 2), gp_sub4(ca[gi], 0), acc, 0, 0, 0);  // hh + lh
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_sub4(wc, 0), gp_sub4(ca[gi], 2), acc, 0, 0, 0);  // mh + hm
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_sub4(wc, 0), gp_sub4(ca[gi], 4), acc, 0, 0, 0);  // mm + hl
+        } else {
+          const gp_u32x4 b0 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768);
+          const gp_u32x4 b1 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768 + 256);
+          const gp_u32x4 b2 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768 + 512);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(b0), gp_op(qa[gi][0]), acc, 0, 0, 0);  // mm + hh
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(b1), gp_op(qa[gi][0]), acc, 0, 0, 0);  // mh + hm
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(b2), gp_op(qa[gi][1]), acc, 0, 0, 0);  // lh + hl
+        }
       }
       // the previous tile's 4 float4 stores, one every G / 4 groups
       if (live && ct > ct0 && DIAG != 2 && gi % (G / 4) == 0) epilogue(accp, ct - 1, gi / (G / 4));
@@ -175,6 +201,15 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
 }
 
 }  // namespace
+
+// KRRN_PANEL_CHAIN=1: the chain weight layout (ops.gemm_weights_panel_chain) and kernel form
+static bool krrn_panel_chain() {
+  static const bool on = [] {
+    const char* e = getenv("KRRN_PANEL_CHAIN");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
 
 KRRN_API int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N, const void* wpf, const float* bias,
                                     const float* res, int ldr, float* out, int ldo, int relu, int csplit,
@@ -203,6 +238,14 @@ KRRN_API int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N
     const char* e = getenv("KRRN_PANEL_DIAG");
     return e ? atoi(e) : 0;
   }();
+  if (krrn_panel_chain()) {
+    if (K == 128 && diag == 1) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 1, true>), grid, dim3(512), 0, s, g);
+    else if (K == 128 && diag == 2) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 2, true>), grid, dim3(512), 0, s, g);
+    else if (K == 128) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 0, true>), grid, dim3(512), 0, s, g);
+    else if (res) hipLaunchKernelGGL((gemm_plds_x3_kernel<64, true, 0, true>), grid, dim3(512), 0, s, g);
+    else hipLaunchKernelGGL((gemm_plds_x3_kernel<64, false, 0, true>), grid, dim3(512), 0, s, g);
+    return krrn_launch_status();
+  }
   if (K == 128 && diag == 1) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 1>), grid, dim3(512), 0, s, g);
   else if (K == 128 && diag == 2) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 2>), grid, dim3(512), 0, s, g);
   else if (K == 128) hipLaunchKernelGGL((gemm_plds_x3_kernel<128, false, 0>), grid, dim3(512), 0, s, g);
