@@ -25,6 +25,8 @@
 
 namespace {
 
+constexpr int kPanelMaxN = 2048;  // columns whose bias a block stages in LDS
+
 typedef __bf16 gp_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 gp_bf16x2 __attribute__((ext_vector_type(2)));
 typedef float gp_f32x2 __attribute__((ext_vector_type(2)));
@@ -50,6 +52,7 @@ __device__ __forceinline__ gp_bf16x8 gp_op(const gp_u32x4 v) { return __builtin_
 // (The round-3 register-only form without the LDS ring re-streamed 768 KB of weight fragments per
 // wave from L2, 3 GB per level-0 launch, and was removed in round 4.)
 typedef unsigned gp_u32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned gp_u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ gp_bf16x8 gp_sub4(const gp_u32x8& c, int o) {
   return __builtin_bit_cast(gp_bf16x8, gp_u32x4{c[o], c[o + 1], c[o + 2], c[o + 3]});
 }
@@ -113,6 +116,11 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
     for (int i = 0; i < PIECES; ++i)
       if (P4 % 512 == 0 || tid + i * 512 < P4) dst[tid + i * 512] = stg[i];
   };
+  // the bias in LDS: a global load inside the store loop would wait (vmcnt counts in order) for every
+  // store issued before it, serialising the write stream with the MFMAs (measured: 211 us = 105 us
+  // without the stores + 86 us without the MFMAs, level-0 GCN GEMM)
+  __shared__ float sbias[kPanelMaxN];
+  for (int n = ct0 * 32 + tid; n < ct1 * 32; n += 512) sbias[n] = g.bias ? g.bias[n] : 0.f;
   if (ct0 < ct1) {
     load_tile(ct0);
     store_tile(0);
@@ -133,13 +141,14 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
   float* orow = g.out + (size_t)(m0 + mrow) * g.ldo;
   const float* rrow = RES ? g.res + (size_t)(m0 + mrow) * g.ldr : nullptr;
   const bool row_ok = mrow < rows_left;
+  f32x4 rv[RES ? 4 : 1];  // the previous tile's residual quads, loaded before this tile's stores
   auto epilogue = [&](const f32x16& acc, int ctp, int q) {
     if (!row_ok) return;
     const int n = ctp * 32 + 8 * q + 4 * fh;
     f32x4 v = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
     if (g.vec) {
-      if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + n);
-      if constexpr (RES) v += *reinterpret_cast<const f32x4*>(rrow + n);
+      v += *reinterpret_cast<const f32x4*>(sbias + n);
+      if constexpr (RES) v += rv[q];
       if (g.relu) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -148,7 +157,7 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float x = v[e] + (g.bias ? g.bias[n + e] : 0.f);
+        float x = v[e] + sbias[n + e];
         if constexpr (RES) x += rrow[n + e];
         if (g.relu) x = fmaxf(x, 0.f);
         orow[n + e] = x;
@@ -162,20 +171,42 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
     const int buf = (ct - ct0) & 1;
     const bool has = ct < ct1;
     if (ct + 1 < ct1) load_tile(ct + 1);  // in flight under this tile's MFMAs
+    if constexpr (RES) {
+      if (g.vec && live && row_ok && ct > ct0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rv[q] = *reinterpret_cast<const f32x4*>(rrow + (ct - 1) * 32 + 8 * q + 4 * fh);
+      }
+    }
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const unsigned* bp = sb[buf] + lane * 4;
+    // CH: group gi + 1's weights are read from LDS while group gi's MFMAs issue (one group ahead,
+    // pinned with sched_barrier: letting the scheduler hoist all 16 groups' reads spilled)
+    gp_u32x4 mh_c;
+    gp_u32x2 lp_c;
+    auto read_w = [&](int gi, gp_u32x4& mh, gp_u32x2& lp) {
+      mh = *reinterpret_cast<const gp_u32x4*>(bp + gi * 384);  // [m h]
+      lp = *reinterpret_cast<const gp_u32x2*>(sb[buf] + gi * 384 + 256 + lane * 2);
+    };
+    if constexpr (CH) {
+      if (live && has && DIAG != 1) read_w(0, mh_c, lp_c);
+    }
 #pragma unroll
     for (int gi = 0; gi < G; ++gi) {
       if (live && has && DIAG != 1) {
         if constexpr (CH) {
-          const gp_u32x4 mh = *reinterpret_cast<const gp_u32x4*>(bp + gi * 384);
-          const unsigned* lp = sb[buf] + gi * 384 + 256 + lane * 2;
-          const gp_u32x8 wc = {mh[0], mh[1], mh[2], mh[3], lp[0], lp[1], 0u, 0u};  // [m h l]
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_sub4(wc, 2), gp_sub4(ca[gi], 0), acc, 0, 0, 0);  // hh + lh
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_sub4(wc, 0), gp_sub4(ca[gi], 2), acc, 0, 0, 0);  // mh + hm
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_sub4(wc, 0), gp_sub4(ca[gi], 4), acc, 0, 0, 0);  // mm + hl
+          gp_u32x4 mh_n;
+          gp_u32x2 lp_n;
+          if (gi + 1 < G) read_w(gi + 1, mh_n, lp_n);
+          const gp_u32x4 hl = {mh_c[2], mh_c[3], lp_c[0], lp_c[1]};  // [h l]
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(hl), gp_sub4(ca[gi], 0), acc, 0, 0, 0);    // hh + lh
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(mh_c), gp_sub4(ca[gi], 2), acc, 0, 0, 0);  // mh + hm
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(mh_c), gp_sub4(ca[gi], 4), acc, 0, 0, 0);  // mm + hl
+          if (gi + 1 < G) {
+            mh_c = mh_n;
+            lp_c = lp_n;
+          }
         } else {
           const gp_u32x4 b0 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768);
           const gp_u32x4 b1 = *reinterpret_cast<const gp_u32x4*>(bp + gi * 768 + 256);
@@ -187,6 +218,7 @@ __global__ __launch_bounds__(512, 1) void gemm_plds_x3_kernel(const PanelArgs g)
       }
       // the previous tile's 4 float4 stores, one every G / 4 groups
       if (live && ct > ct0 && DIAG != 2 && gi % (G / 4) == 0) epilogue(accp, ct - 1, gi / (G / 4));
+      if constexpr (CH) __builtin_amdgcn_sched_barrier(0);
     }
     if (DIAG == 2 && live) {
       float sum = 0.f;
@@ -215,7 +247,7 @@ KRRN_API int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N
                                     const float* res, int ldr, float* out, int ldo, int relu, int csplit,
                                     void* stream) {
   if (!a || !wpf || !out) return KRRN_EARG;
-  if (M < 1 || (K != 64 && K != 128) || N < 32 || (N & 31) || csplit < 1) return KRRN_ESHAPE;
+  if (M < 1 || (K != 64 && K != 128) || N < 32 || (N & 31) || N > kPanelMaxN || csplit < 1) return KRRN_ESHAPE;
   if (lda < K || ldo < N || (res && ldr < N)) return KRRN_ESHAPE;
   if ((lda & 3) || !krrn_aligned16(a) || !krrn_aligned16(wpf)) return KRRN_EALIGN;
   const int ntiles = N >> 5;
