@@ -312,7 +312,7 @@ def quad_weights_x3(wt: torch.Tensor, N: int, K: int, kq_mult: int = 4) -> torch
     return torch.cat([mh, lp]).contiguous()
 
 
-PANEL_CHAIN = os.environ.get("KRRN_PANEL_CHAIN", "0") == "1"
+PANEL_CHAIN = os.environ.get("KRRN_PANEL_CHAIN", "0") == "1" or os.environ.get("KRRN_PANEL_DMA", "0") == "1"
 
 
 def gemm_weights_panel_chain(wt: torch.Tensor) -> torch.Tensor:
