@@ -150,11 +150,11 @@ int krrn_gemm_x3_gather_f32(const int* ia, const float* A, long long a_bs, int a
  * N = 8 * 128) and layer1's 64 -> 256 1x1 convs (myhrnet.py:65-103, K = 64):
  *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n][k] + bias[n] + res[m*ldr + n]),  0 <= n < N
  * Split-bf16 operands at f32 accuracy; each wave keeps its 32 activation rows in registers, the
- * 8 waves of a block walk 32-column tiles whose weights are staged once per block in LDS. wpf
- * holds W split into per-wave fragments (ops.gemm_weights_panel: [N/32][K/8][3][64 lanes][4] u32;
- * with KRRN_PANEL_CHAIN=1 the chain layout of ops.gemm_weights_panel_chain, [N/32][K/8][384] u32).
+ * 4 waves of a block walk 32-column tiles whose weights are copied once per block into LDS. wpf
+ * holds W split into bf16 terms (ops.gemm_weights_panel: [N/32][K/8][384] u32, per 8-k group 64 lanes
+ * x [m0..m3 h0..h3] then 64 lanes x [l0..l3]).
  * K = 64 or 128, N % 32 == 0, N <= 2048, lda % 4 == 0, A / wpf 16-byte
- * aligned; `csplit` column ranges per row panel (grid = ceil(M / 256) x csplit). K = 128 with a
+ * aligned; `csplit` column ranges per row panel (grid = ceil(M / 128) x csplit). K = 128 with a
  * residual: KRRN_EUNSUPPORTED. */
 int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N, const void* wpf, const float* bias,
                            const float* res, int ldr, float* out, int ldo, int relu, int csplit, void* stream);

@@ -312,12 +312,9 @@ def quad_weights_x3(wt: torch.Tensor, N: int, K: int, kq_mult: int = 4) -> torch
     return torch.cat([mh, lp]).contiguous()
 
 
-PANEL_CHAIN = os.environ.get("KRRN_PANEL_CHAIN", "0") == "1" or os.environ.get("KRRN_PANEL_DMA", "0") == "1"
-
-
-def gemm_weights_panel_chain(wt: torch.Tensor) -> torch.Tensor:
-    """GEMM weights [N][K] f32 (scale folded) -> the chain layout of krrn_gemm_panel_x3_f32 under
-    KRRN_PANEL_CHAIN=1: int32 [N/32][K/8][384]; per (column tile nb, 8-k group g) 64 lanes x [m0..m3
+def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:
+    """GEMM weights [N][K] f32 (scale folded) -> the layout krrn_gemm_panel_x3_f32 reads: int32
+    [N/32][K/8][384]; per (column tile nb, 8-k group g) 64 lanes x [m0..m3
     h0..h3] (256 words) then 64 lanes x [l0..l3] (128 words), lane fh*32 + nl = column 32 nb + nl,
     k = 8 g + 4 fh .. + 3. N % 32 == 0, K % 8 == 0."""
     N, K = wt.shape
@@ -326,21 +323,6 @@ def gemm_weights_panel_chain(wt: torch.Tensor) -> torch.Tensor:
     mh = mh.reshape(N // 32, 32, K // 8, 2, 4).permute(0, 2, 3, 1, 4)        # nb g fh nl 4
     lp = l.contiguous().view(torch.int32).reshape(N // 32, 32, K // 8, 2, 2).permute(0, 2, 3, 1, 4)
     return torch.cat([mh.reshape(N // 32, K // 8, 256), lp.reshape(N // 32, K // 8, 128)], dim=-1).contiguous()
-
-
-def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:
-    """GEMM weights [N][K] f32 (scale folded) -> the wave fragments krrn_gemm_panel_x3_f32 reads: int32
-    [N/32][K/8][3][64][4]. Fragment (column tile nb, 8-k group g, quad q) is one coalesced 1-KB wave
-    load: lane fh*32 + nl holds, for column 32 nb + nl and k = 8 g + 4 fh .. + 3, the quad q of the
-    split terms: q = 0 [h0..h3 m0..m3] (x the activations' [h m]: hh + mm), q = 1 [m0..m3 h0..h3]
-    (x [h m]: hm + mh), q = 2 [l0..l3 h0..h3] (x [h l]: hl + lh). N % 32 == 0, K % 8 == 0."""
-    if PANEL_CHAIN:
-        return gemm_weights_panel_chain(wt)
-    N, K = wt.shape
-    h, m, l = (t.reshape(N, K // 4, 4) for t in split_bf16x3(wt))
-    c = torch.cat([h, m, m, h, l, h], dim=-1).contiguous()  # [N][K/4][24] bf16 = q0 | q1 | q2
-    c = c.view(torch.int32).reshape(N // 32, 32, K // 8, 2, 3, 4)  # nb nl g fh q 4
-    return c.permute(0, 2, 4, 3, 1, 5).contiguous()                 # nb g q fh nl 4
 
 
 def wino_eligible(spec: ConvSpec, M: int) -> bool:

@@ -24,13 +24,13 @@ def test_kchunk_weights_order():
 
 
 def test_panel_chain_layout_reconstructs_weights():
-    """ops.gemm_weights_panel_chain: word (nb, g, lane, i) of the [m h] plane and (nb, g, lane, j) of
+    """ops.gemm_weights_panel: word (nb, g, lane, i) of the [m h] plane and (nb, g, lane, j) of
     the [l] plane hold the split terms of W[32 nb + lane % 32, 8 g + 4 (lane / 32) + e], and
     h + m + l == W exactly."""
     g = torch.Generator().manual_seed(0)
     N, K = 64, 32
     W = torch.randn(N, K, generator=g)
-    P = ops.gemm_weights_panel_chain(W)
+    P = ops.gemm_weights_panel(W)
     assert P.shape == (N // 32, K // 8, 384) and P.dtype == torch.int32
     mh = P[..., :256].reshape(N // 32, K // 8, 64, 4)
     lp = P[..., 256:].reshape(N // 32, K // 8, 64, 2)
