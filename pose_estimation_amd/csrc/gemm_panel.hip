@@ -105,23 +105,17 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
   const int ct0 = blockIdx.y * g.ntile_per_split;
   const int ct1 = min(ct0 + g.ntile_per_split, g.N >> 5);
   for (int n = ct0 * 32 + tid; n < ct1 * 32; n += 256) sbias[n] = g.bias ? g.bias[n] : 0.f;
-  // this wave's NI 1-KB pieces of tile ct: byte offset (ct * TILE_U32 + (wave * NI + i) * 256) * 4
-  // of the weights, per-lane voffset lane * 16, the rest in soffset. Issued as inline asm: through the
-  // builtin the compiler cannot tell the ring halves apart and waits (vmcnt(0)) for the DMA into one
-  // before reading the other, and for every store before each barrier; completion is handled here
-  // (the explicit vmcnt before the barrier below)
-  const unsigned long long wbase = (unsigned long long)g.w;
-  const gp_u32x4 wdesc = {(unsigned)wbase, (unsigned)(wbase >> 32) & 0xFFFFu,
-                          (unsigned)min((long long)(g.N >> 5) * TILE_U32 * 4, 0x7FFFFFFFLL), 0x00020000u};
-  const unsigned voff = (unsigned)(lane * 16);
+  // this wave's NI 1-KB pieces of tile ct: byte offset (ct * TILE_U32 + (wave * NI + i) * 256) * 4,
+  // through a buffer resource (per-lane 32-bit voffset, the tile part in soffset: no 64-bit address
+  // registers)
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.w, (short)0, (int)min((long long)(g.N >> 5) * TILE_U32 * 4, 0x7FFFFFFFLL), 0x00020000);
   auto dma_tile = [&](int ct, unsigned* dst) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const unsigned lds = (unsigned)(unsigned long)(gp_lds_void*)(dst + (wave * NI + i) * 256);
-      const unsigned soff = (unsigned)((ct * TILE_U32 + (wave * NI + i) * 256) * 4);
-      asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                   :: "s"(lds), "v"(voff), "s"(wdesc), "s"(soff) : "memory");
-    }
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (gp_lds_void*)(dst + (wave * NI + i) * 256), 16,
+                                               (unsigned)(lane * 16),
+                                               (unsigned)((ct * TILE_U32 + (wave * NI + i) * 256) * 4), 0, 0);
   };
   if (ct0 < ct1) dma_tile(ct0, sbA);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
