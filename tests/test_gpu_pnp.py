@@ -217,12 +217,18 @@ def test_full_ransac_matches_oracle(dev, noise_px, outliers):
 def test_ransac_matches_opencv_semantics_oracle(dev, noise_px, pose_tol):
     """Against oracle_pnp_ransac_cv, the restatement that follows OpenCV's epnp.cpp numerics instead
     of the kernel's (cyclic 12 x 12 Jacobi, SVD beta solves, QR Gauss-Newton, U V^T with OpenCV's det
-    fix, sequential sums) on the same subsets: the inlier count within 8 and R / t within 1e-4
-    noiseless, 1e-2 with 0.4 px noise (the tolerances of the round-2 test against an SVD-based
+    fix, sequential sums) on the same subsets: the inlier count within 8 (with noise: not below the
+    oracle's by more than 8) and R / t within 1e-4 noiseless, 1e-2 with 0.4 px noise (the tolerances of the round-2 test against an SVD-based
     oracle; the bit-order comparison is test_full_ransac_matches_oracle)."""
     B, N, S = 16, 1000, 100
     xyz, data, _, _ = _scene(B, N, S, 9, outlier_frac=0.3, noise_px=noise_px)
-    R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, return_info=True)
+    # the 256-point selection and the hypothesis subsets from a local generator: the test does not
+    # depend on how far earlier tests moved the global CPU / device RNG streams
+    g = torch.Generator().manual_seed(2024)
+    sel0 = torch.stack([torch.randperm(N, generator=g)[:256] for _ in range(B)]).to(torch.int32)
+    subs0 = torch.stack([torch.stack([torch.randperm(256, generator=g)[:5] for _ in range(100)])
+                         for _ in range(B)]).to(torch.int32)
+    R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, sel=sel0, subsets=subs0, return_info=True)
     torch.cuda.synchronize()
     sel = info["sel"].cpu().long()
     subs = info["subsets"].cpu()
@@ -233,7 +239,12 @@ def test_ransac_matches_opencv_semantics_oracle(dev, noise_px, pose_tol):
         obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
         img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
         Ro, to, cnt, _ = opnp.pnp_ransac_cv(obj, img, K4, subs[b].numpy(), 1.0)
-        assert abs(int(info["inliers"][b]) - cnt) <= 8, (b, int(info["inliers"][b]), cnt)
+        # noiseless: the same count within 8; with noise the two numerics can pick different
+        # hypotheses of the same 100, so the GPU's RANSAC must be at least as good (count >= oracle - 8)
+        if noise_px == 0:
+            assert abs(int(info["inliers"][b]) - cnt) <= 8, (b, int(info["inliers"][b]), cnt)
+        else:
+            assert int(info["inliers"][b]) >= cnt - 8, (b, int(info["inliers"][b]), cnt)
         worst = max(worst, float(np.abs(R[b].cpu().numpy() - Ro).max()), float(np.abs(t[b].cpu().numpy() - to).max()))
     print(f"noise {noise_px} px: max |dR|, |dt| vs the OpenCV-semantics oracle {worst:.2e}")
     assert worst < pose_tol, worst
