@@ -32,6 +32,16 @@ struct Cam {
   double fu, fv, uc, vc;
 };
 
+// Scheduling fence: the values are "rewritten" by an empty asm, so nothing computed after this
+// point moves above it. Without these, LLVM moved the eigenvector updates (U <- U J, independent of
+// the A chain) of many rotations together and held their intermediate values: the hypothesis kernel
+// needed 446 registers (one wave per SIMD); with them 256 (two).
+template <int N>
+__device__ __forceinline__ void fence_regs(double (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
 // ---- small symmetric eigen-solves in registers --------------------------------------------
 // A (destroyed) -> eigenvalues w (descending) and eigenvectors as ROWS of V.
 template <int N>
@@ -81,6 +91,8 @@ __device__ __forceinline__ void eig_small(double (&A)[N * N], double (&w)[N], do
           U[k * N + p] = c * ukp - s * ukq;
           U[k * N + q] = s * ukp + c * ukq;
         }
+        fence_regs(U);
+        fence_regs(A);
       }
     }
   }
@@ -231,6 +243,8 @@ __device__ __forceinline__ void eig12_rows(const double (&row)[12], double (&vq)
         u[pp[i]] = cs[i] * xp - ss[i] * xq;
         u[qq[i]] = ss[i] * xp + cs[i] * xq;
       }
+      fence_regs(u);
+      fence_regs(a);
     }
   }
   double w[12];
@@ -278,6 +292,7 @@ __device__ __forceinline__ void lsq_rows(const double (&arow)[N], double brow, d
       for (int j = 0; j < N; ++j) AtA[i * N + j] += ak[i] * ak[j];
       Atb[i] += ak[i] * bk;
     }
+    fence_regs(AtA);
   }
   double C[N * N];
   double dmax = 0.0;
@@ -602,14 +617,17 @@ __device__ __forceinline__ double r_and_t(const SUM& sum, const double (&vq)[4],
 // EPnP (Lepetit et al. 2009) over the points of `sum`, spread over an aligned 16-lane group: the
 // point sums and the small dense algebra replicated in every lane, the rows of M^T M, of the 6 x 10
 // L matrix and of every 6 x N least-squares system one per lane, the 12 x 12 eigen-solve shared
-// (eig12_rows). Result R (row-major), t, identical in every lane of the group.
+// (eig12_rows). Result R (row-major), t as f32 (the precision both callers keep), identical in every
+// lane of the group. The control points and their inverse (cws, ci; 21 values, the same in every lane)
+// live in the group's LDS slot `ctl` after the setup: in registers they were 42 more VGPRs through
+// the whole solve.
 template <class SUM>
-__device__ __forceinline__ void epnp(const SUM& sum, const Cam& cam, double (&Rout)[9], double (&tout)[3]) {
+__device__ __forceinline__ void epnp(const SUM& sum, const Cam& cam, double* ctl, float (&Rout)[9], float (&tout)[3]) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63, r = lane & 15, base = lane & ~15;
   const int n = sum.count();
-  double cws[4][3], ci[9], cw[3];
   {
+    double cws[4][3], ci[9], cw[3];
     sum([&](const double* X, const double*, double (&acc)[3]) {
           acc[0] += X[0]; acc[1] += X[1]; acc[2] += X[2];
         }, cw);
@@ -640,7 +658,15 @@ __device__ __forceinline__ void epnp(const SUM& sum, const Cam& cam, double (&Ro
     pinv3(CC, CI);
 #pragma unroll
     for (int i = 0; i < 9; ++i) ci[i] = CI[i];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) ctl[j] = cws[j / 3][j % 3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) ctl[12 + i] = ci[i];
   }
+  asm volatile("" ::: "memory");  // read back from LDS below, not forwarded in registers
+  const double(*cws)[3] = reinterpret_cast<const double(*)[3]>(ctl);
+  const double* ci = ctl + 12;
+  const double* cw = ctl;  // cws[0] is the centroid
   double vq[4];
   {
     double mrow[12];
@@ -681,6 +707,7 @@ __device__ __forceinline__ void epnp(const SUM& sum, const Cam& cam, double (&Ro
   double best_err = 1e300;
 #pragma unroll 1
   for (int approx = 1; approx <= 3; ++approx) {
+    asm volatile("" ::: "memory");  // keeps the LDS reads of cws / ci in the loop body
     double betas[4] = {0, 0, 0, 0};
     if (approx == 1) {
       const double arow[4] = {Lr[0], Lr[1], Lr[3], Lr[6]};
@@ -727,9 +754,9 @@ __device__ __forceinline__ void epnp(const SUM& sum, const Cam& cam, double (&Ro
     if (approx == 1 || err < best_err) {
       best_err = err;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) Rout[i] = R[i];
+      for (int i = 0; i < 9; ++i) Rout[i] = (float)R[i];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) tout[i] = t[i];
+      for (int i = 0; i < 3; ++i) tout[i] = (float)t[i];
     }
   }
 }
@@ -771,12 +798,13 @@ __device__ void load_corr(int b, const float* xyz, int HW, const long long* choo
 // the P correspondences only (5 KB at P = 256), so the blocks co-reside with the fusion / TBase
 // launches they run beside; no scratch memory (every register array has compile-time indices).
 template <int kHypPerBlock>
-__global__ __launch_bounds__(16 * kHypPerBlock) void pnp_hyp_kernel(
+__global__ __launch_bounds__(16 * kHypPerBlock, 2) void pnp_hyp_kernel(
     const float* __restrict__ xyz, int HW, const long long* __restrict__ choose, int N, const int* __restrict__ sel,
     int P, const float* __restrict__ xmap, const float* __restrict__ ymap, const float* __restrict__ K4,
     const double* __restrict__ extent, const double* __restrict__ lfb, const int* __restrict__ subsets, int H,
     float thr, float* __restrict__ hyp_pose, int* __restrict__ hyp_cnt) {
   extern __shared__ float pnp_corr[];
+  __shared__ double sctl[kHypPerBlock][24];
   float* sobj = pnp_corr;
   float* simg = sobj + 3 * P;
   const int b = blockIdx.x;
@@ -791,13 +819,8 @@ __global__ __launch_bounds__(16 * kHypPerBlock) void pnp_hyp_kernel(
   sub.img = simg;
 #pragma unroll
   for (int i = 0; i < 5; ++i) sub.ids[i] = subsets[((long long)b * H + hs) * 5 + i];
-  double R[9], t[3];
-  epnp(sub, cam, R, t);
   float Rf[9], tf[3];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Rf[i] = (float)R[i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) tf[i] = (float)t[i];
+  epnp(sub, cam, sctl[threadIdx.x >> 4], Rf, tf);
   const float thr2 = thr * thr;
   int cnt = 0;
   for (int p = r; p < P; p += 16) cnt += is_inlier(Rf, tf, sobj + 3 * p, simg + 2 * p, cam, thr2) ? 1 : 0;
@@ -839,6 +862,7 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
   __shared__ float sobj[kPnpMaxP * 3];
   __shared__ float simg[kPnpMaxP * 2];
   __shared__ int slist[kPnpMaxP];
+  __shared__ double sctl[4][24];
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const Cam cam = {K4[4 * b + 0], K4[4 * b + 1], K4[4 * b + 2], K4[4 * b + 3]};
@@ -881,13 +905,13 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
   __syncthreads();
   if (ok && n >= 5) {
     const WaveSum inl{sobj, simg, slist, n};
-    double R[9], t[3];
-    epnp(inl, cam, R, t);
+    float R[9], t[3];
+    epnp(inl, cam, sctl[lane >> 4], R, t);
     if (lane == 0) {
 #pragma unroll
-      for (int i = 0; i < 9; ++i) Rout[9 * b + i] = (float)R[i];
+      for (int i = 0; i < 9; ++i) Rout[9 * b + i] = R[i];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) tout[3 * b + i] = (float)t[i];
+      for (int i = 0; i < 3; ++i) tout[3 * b + i] = t[i];
     }
   } else if (lane == 0) {
     // RANSAC failed (< 5 inliers): cv::solvePnPRansac returns false with rvec = tvec = 0,
