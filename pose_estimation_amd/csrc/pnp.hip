@@ -171,12 +171,23 @@ __device__ __forceinline__ double group_sum16(double v) {
   return v;
 }
 
+typedef double pnp_d2 __attribute__((ext_vector_type(2)));
+
 // In: lane r's row of M^T M (zero in lanes 12..15). Out: vq[q] = component r of the eigenvector of
 // the q-th smallest eigenvalue (ascending, ties: lower column first) -- each lane keeps its own
 // components only (the old form broadcast all 48 into every lane: 96 VGPRs).
-__device__ __forceinline__ void eig12_rows(const double (&row)[12], double (&vq)[4]) {
+// The per-step exchanges go through the group's LDS area xs (kPnpXs doubles, 16-B aligned): lane r
+// writes its row at the step's start (then reads a[r][r], a[p][p], a[lo][hi] at per-lane addresses:
+// two 12-way select chains before), its (c, s) (then reads the 6 pairs' (c, s)), and its row after
+// A <- A J (then reads the partner's): 6 + 3 / 1 + 6 / 6 + 6 accesses per step where lane shuffles
+// took 4 / 24 / 24 ds_bpermute. Lanes of one wave: the hardware keeps a wave's LDS accesses in
+// order, and the wave barriers keep the compiler from moving them.
+constexpr int kPnpXs = 16 * 12 + 16 * 2;
+__device__ __forceinline__ void eig12_rows(const double (&row)[12], double (&vq)[4], double* xs) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63, r = lane & 15, base = lane & ~15;
+  double* const xrow = xs;             // [16][12]
+  double* const xcs = xs + 16 * 12;    // [16][2]: (c, s)
   const bool act = r < 12;
   double a[12], u[12];
 #pragma unroll
@@ -201,9 +212,16 @@ __device__ __forceinline__ void eig12_rows(const double (&row)[12], double (&vq)
     for (int k = 0; k < 11; ++k) {
       const int pr = act ? rr_partner(k, r) : r;
       const int lo = r < pr ? r : pr;
-      const double d = pick(a, r);                            // own diagonal
-      const double apq = shfl_f64(pick(a, pr), base + lo);    // a[lo][hi], from lane lo
-      const double dp = shfl_f64(d, base + pr);               // partner's diagonal
+      // the step's inputs from the rows in LDS (per-lane addresses instead of select chains over a[])
+#pragma unroll
+      for (int j = 0; j < 12; j += 2) *reinterpret_cast<pnp_d2*>(xrow + 12 * r + j) = pnp_d2{a[j], a[j + 1]};
+      __builtin_amdgcn_wave_barrier();
+      const int hi = r < pr ? pr : r;
+      const int rc = act ? r : 11, pc = act ? pr : 11;        // idle lanes 12..15 read a valid slot
+      const double d = xrow[13 * rc];                         // own diagonal
+      const double dp = xrow[13 * pc];                        // partner's diagonal
+      const double apq = act ? xrow[12 * lo + hi] : 0.0;      // a[lo][hi], lane lo's row
+      __builtin_amdgcn_wave_barrier();
       const double app = r == lo ? d : dp, aqq = r == lo ? dp : d;
       double c = 1.0, sn = 0.0;
       if (act && !(fabs(apq) < 1e-300 || fabs(apq) < 1e-18 * sqrt(fabs(app * aqq)))) {
@@ -215,13 +233,16 @@ __device__ __forceinline__ void eig12_rows(const double (&row)[12], double (&vq)
       // the 6 pairs of step k: (k, 11) and ((k + i) % 11, (k - i) % 11), i = 1..5; (c, s) from the lower lane
       double cs[6], ss[6];
       int pp[6], qq[6];
+      *reinterpret_cast<pnp_d2*>(xcs + 2 * r) = pnp_d2{c, sn};
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         const int x = i == 0 ? k : (k + i) % 11, y = i == 0 ? 11 : (k - i + 11) % 11;
         pp[i] = x < y ? x : y;
         qq[i] = x < y ? y : x;
-        cs[i] = shfl_f64(c, base + pp[i]);
-        ss[i] = shfl_f64(sn, base + pp[i]);
+        const pnp_d2 v = *reinterpret_cast<const pnp_d2*>(xcs + 2 * pp[i]);
+        cs[i] = v.x;
+        ss[i] = v.y;
       }
       // A <- A J: own row, columns (p_i, q_i)
 #pragma unroll
@@ -232,9 +253,16 @@ __device__ __forceinline__ void eig12_rows(const double (&row)[12], double (&vq)
       }
       // A <- J^T A: row lo' = c row lo - s row hi, row hi' = s row lo + c row hi
 #pragma unroll
-      for (int j = 0; j < 12; ++j) {
-        const double y = shfl_f64(a[j], base + pr);
-        a[j] = r == lo ? c * a[j] - sn * y : sn * y + c * a[j];
+      for (int j = 0; j < 12; j += 2) *reinterpret_cast<pnp_d2*>(xrow + 12 * r + j) = pnp_d2{a[j], a[j + 1]};
+      __builtin_amdgcn_wave_barrier();
+      // c a - s y (lane lo) and s y + c a (lane hi) as c a + s' y, s' = -s / s: the same IEEE results
+      // (negation and the order of two addends are exact), no per-element select
+      const double sgn_s = r == lo ? -sn : sn;
+#pragma unroll
+      for (int j = 0; j < 12; j += 2) {
+        const pnp_d2 y = *reinterpret_cast<const pnp_d2*>(xrow + 12 * pr + j);
+        a[j] = c * a[j] + sgn_s * y.x;
+        a[j + 1] = c * a[j + 1] + sgn_s * y.y;
       }
       // U <- U J
 #pragma unroll
@@ -671,7 +699,7 @@ __device__ __forceinline__ void epnp(const SUM& sum, const Cam& cam, double* ctl
   {
     double mrow[12];
     sum.rows(cws, ci, cam, mrow);
-    eig12_rows(mrow, vq);
+    eig12_rows(mrow, vq, ctl + 32);
   }
   // lane i < 6: row i of L (6 x 10) and rho[i]; pair (a, b) of control points per row
   const int li = r < 6 ? r : 5;
@@ -804,7 +832,7 @@ __global__ __launch_bounds__(16 * kHypPerBlock, 2) void pnp_hyp_kernel(
     const double* __restrict__ extent, const double* __restrict__ lfb, const int* __restrict__ subsets, int H,
     float thr, float* __restrict__ hyp_pose, int* __restrict__ hyp_cnt) {
   extern __shared__ float pnp_corr[];
-  __shared__ double sctl[kHypPerBlock][24];
+  __shared__ __attribute__((aligned(16))) double sctl[kHypPerBlock][32 + kPnpXs];
   float* sobj = pnp_corr;
   float* simg = sobj + 3 * P;
   const int b = blockIdx.x;
@@ -862,7 +890,7 @@ __global__ __launch_bounds__(64) void pnp_refine_kernel(
   __shared__ float sobj[kPnpMaxP * 3];
   __shared__ float simg[kPnpMaxP * 2];
   __shared__ int slist[kPnpMaxP];
-  __shared__ double sctl[4][24];
+  __shared__ __attribute__((aligned(16))) double sctl[4][32 + kPnpXs];
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const Cam cam = {K4[4 * b + 0], K4[4 * b + 1], K4[4 * b + 2], K4[4 * b + 3]};
