@@ -443,7 +443,6 @@ struct HypSum {
   const float* obj;  // LDS [P][3]
   const float* img;  // LDS [P][2]
   int ids[5];
-  static constexpr int n = 5;
   __device__ __forceinline__ void pt(int i, double* X, double* q) const {
     const float* o = obj + 3 * ids[i];
     X[0] = o[0]; X[1] = o[1]; X[2] = o[2];
