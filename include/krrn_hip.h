@@ -193,20 +193,6 @@ int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, i
 int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* U3,
                              int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                              int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
-/* Kernel choice for krrn_conv3x3_wino_x3_f32 (process-wide; env KRRN_WINO_X3W): 0 = 32 output tiles
- * x 64 channels per block at two waves per SIMD, 1 = 64 tiles x 64 channels per block at one wave per
- * SIMD (accumulators in the AccVGPR file, half the weight bytes per MFMA). Bit-identical results. */
-int krrn_wino_x3_variant(int v);
-/* conv3x3(UpsamplingBilinear2d(scale 2)(in)) fused (krrn.py:56-57 / 78-79: XYZNet's / NMLNet's x2
- * upsample, align_corners=True, followed by a 3x3 conv + BN + ReLU): in is the Hs x Ws source
- * (NHWC, channel stride / offset in_cs / in_co), the conv runs on the 2Hs x 2Ws upsample without
- * writing it -- the kernel blends each up-sampled pixel from its 4 source pixels while staging its
- * Winograd input (the expression of krrn_resize_bilinear_f32, bit-identical), on the one-wave-per-
- * SIMD split-bf16 Winograd kernel. U3, epilogue and output (2Hs x 2Ws) as krrn_conv3x3_wino_x3_f32.
- * Hs, Ws >= 2; in 16-byte aligned. */
-int krrn_conv3x3_wino_x3_up2_f32(const float* in, int in_cs, int in_co, int B, int Hs, int Ws, int cin, const void* U3,
-                                 int N, int n_store, const float* scale, const float* bias, const float* res,
-                                 int res_cs, int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
 
 /* Direct conv for narrow layers: 3x3 / pad 1 / stride 1 or 2, or 1x1 / stride 1 (the HRNet
  * branches' BasicBlock convs, lib/network/hrnet/myhrnet.py:34-63, and the fuse layers' stride-2

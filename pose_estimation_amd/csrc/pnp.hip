@@ -429,7 +429,11 @@ __device__ __forceinline__ void mtm_row_add(const double* X, const double* q, co
     r2[3 * j + 1] = a[j] * cam.fv;
     r2[3 * j + 2] = a[j] * (cam.vc - q[1]);
   }
-  const double r1r = pick(r1, r), r2r = pick(r2, r);
+  // r1[r], r2[r] from a[r / 3] (a 4-way select, not two 12-way ones; the same products)
+  const int jr = r / 3, tr = r - 3 * jr;
+  const double aj = pick(a, jr);
+  const double r1r = tr == 0 ? aj * cam.fu : (tr == 1 ? 0.0 : aj * (cam.uc - q[0]));
+  const double r2r = tr == 0 ? 0.0 : (tr == 1 ? aj * cam.fv : aj * (cam.vc - q[1]));
 #pragma unroll
   for (int j = 0; j < 12; ++j) acc[j] += r1r * r1[j] + r2r * r2[j];
 }

@@ -26,7 +26,7 @@
 // one chunk ahead. One barrier per chunk. The output transform: wave w holds row u = w of every
 // (tile, channel)'s 4x4 M, so the column combination is lane-local and only 2 of 4 values per
 // row go through LDS; stores are float4 channel runs. The step runs the split-bf16 forms below
-// (wino_f23_x3_kernel, wino_f23_x3w_kernel); this f32 kernel is their accuracy reference.
+// (wino_f23_x3_kernel); this f32 kernel is its accuracy reference.
 // Round 1's register-staged kernel (every thread transforming one (tile, channel) patch into an
 // LDS image of V, weights staged through LDS, two barriers per chunk: bit-identical, 1.55 ms) and
 // the ring without the transform overlap were removed in round 4.
@@ -74,10 +74,6 @@ struct WinoArgs {
   int relu;
   int vec;        // float4 epilogue (16-B aligned channel runs, n_store % 4 == 0)
   int Ht, Wt, T;  // tiles per column / row, total tiles
-  // fused x2 upsample (wino_f23_x3w_kernel<true>): `in` is the Hs x Ws source, H x W = 2Hs x 2Ws its
-  // align_corners=True bilinear upsample; img counts source-image elements
-  int Hs, Ws;
-  float sh, sw;
 };
 
 // Output transform Y = A^T M A + epilogue. Wave w holds row u = w of the 4x4 component grid
@@ -519,374 +515,7 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
   wino_epi_finish2d(a, smem, b, ty0, tx0, n0);
 }
 
-// ---- Split-bf16 Winograd, one wave per SIMD, 64 tiles per block (wino_f23_x3w_kernel) ---------
-// Why: the 32-tile kernel above streams each chunk's split weights (16 x 64 x 8 x 6 B = 48 KB per
-// block) from L2 for 96 MFMAs: 512 B per MFMA, 64 B per clock per CU at the full matrix rate, above
-// the ~56 B/clk/CU share of the chip's ~34.5 TB/s of L2 bandwidth (MI355X_MICROARCH.md) -- the weight
-// stream, not the matrix pipe, sets its pace (PMC: TA ~72 % busy). Doubling the tiles that share a
-// weight fetch halves that.
-// Block = 16 x 4 output tiles (64 tiles: two 32-tile M-blocks) x 64 output channels, 256 threads,
-// ONE block per CU. Wave w owns component row u = w (xi = 4w .. 4w + 3) over both M-blocks and both
-// 32-channel n-blocks: 2 x 4 x 2 accumulators of 32 x 32 = 256 registers, which only fit with the
-// AccVGPR file (one wave per SIMD: 256 VGPRs + 256 AGPRs). Each split V (one tile row, 4 channels)
-// still feeds both n-blocks, so the VALU per MFMA is the 32-tile kernel's; with one wave per SIMD
-// the split / transform VALU issues between the wave's own MFMAs (v_cvt_pk_bf16_f32 beside an MFMA
-// is free: MI355X_MICROARCH.md constants).
-//   * raw input ring: the block's 10 x 34 pixel x 8 channel region per chunk (680 16-B pieces, 3 per
-//     thread), 3 slots, one barrier per chunk; LDS slot of a piece = h * 484 + (col & 1) * 242 +
-//     row * 24 + col / 2 (16-B units): make_v's ds_read_b128 and the staging ds_write_b128 are
-//     bank-conflict-free (every lane group of the instruction hits 16 distinct 16-B bank slots);
-//   * weights: as the 32-tile kernel (plane U_mh b128 + plane U_l b64 per (v, n-block)), one
-//     buffer (48 VGPRs), component v's reloaded for the next chunk once both M-blocks used them;
-//   * epilogue: the column combination (c0, c1) of every (tile, channel) through LDS (139 KB, the
-//     ring's space), then rows combined with BN / residual / ReLU and float4 channel-run stores.
-// Same V operands, U operands and per-accumulator MFMA order as wino_f23_x3_kernel: bit-identical
-// outputs (tests/test_gpu_conv.py).
-constexpr int kXGX = 16, kXGY = 4, kXT = kXGX * kXGY;  // tiles per block (x, y)
-constexpr int kXRR = 2 * kXGY + 2, kXRC = 2 * kXGX + 2;  // raw region rows / cols
-constexpr int kXPieces = kXRR * kXRC * 2;                // 16-B pieces per chunk
-constexpr int kXPer = (kXPieces + 255) / 256;            // pieces per thread
-constexpr int kXRowP = 24, kXColP = 242, kXHalfP = 484;   // ring layout (16-B units), see above
-constexpr int kXSlot = 2 * kXHalfP;                      // 16-B units per ring slot
-constexpr int kXSP = kWN + 4;                            // epilogue staging pitch (floats)
-constexpr int kXEpi = 4 * 2 * kXT * kXSP;                // epilogue staging floats
-static_assert(kXRC / 2 <= kXRowP && kXRR * kXRowP <= kXColP && 2 * kXColP <= kXHalfP, "ring layout");
-static_assert(3 * kXSlot * 4 <= kXEpi, "ring fits in the epilogue staging");
-static_assert(kWN == 64, "two 32-channel n-blocks per block");
-
-__device__ __forceinline__ int xw_slot(int h, int rr, int rc) {
-  return h * kXHalfP + (rc & 1) * kXColP + rr * kXRowP + (rc >> 1);
-}
-
-// Source region of the fused-upsample form (UP2): the 10 x 34 up-sampled pixels of a block read at
-// most 7 x 19 source pixels (scale (Hs - 1) / (2 Hs - 1) < 1/2: 9 up rows span < 4.5 source rows, so
-// 6 distinct floor rows + the next one; 33 up columns < 16.5 source columns: 18 + 1).
-constexpr int kSR = 7, kSC = 19, kSPieces = kSR * kSC * 2, kSPer = (kSPieces + 255) / 256;
-static_assert(3 * kXSlot + 2 * kSPieces <= kXEpi / 4, "ring + source buffers fit the epilogue staging");
-
-template <bool UP2>
-__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino_f23_x3w_kernel(
-    const WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[kXEpi];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gxn = krrn_cdiv(a.Wt, kXGX), gyn = krrn_cdiv(a.Ht, kXGY), nbn = krrn_cdiv(a.N, kWN);
-  const int per_img = gxn * gyn;
-  const int bid = krrn_xcd_remap(blockIdx.x, a.B * per_img * nbn);
-  const int sp = bid / nbn, nb = bid - (bid / nbn) * nbn;
-  const int b = sp / per_img, r2 = sp - (sp / per_img) * per_img;
-  const int by = r2 / gxn, bx = r2 - (r2 / gxn) * gxn;
-  const int n0 = nb * kWN;
-  const int ty0 = by * kXGY, tx0 = bx * kXGX;
-  const int nck = krrn_cdiv(a.cin, kWC);
-
-  // raw staging: this thread's pieces e = tid + 256 k (pixel e / 2 of the region, channel half e & 1)
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.in + (size_t)b * a.img + a.in_co), (short)0, (int)min(a.img * 4 - (long long)a.in_co * 4, 0x7FFFFFFFLL),
-      0x00020000);
-  int rdst[kXPer];  // LDS 16-B slot in a ring slot, -1: no piece
-#pragma unroll
-  for (int k = 0; k < kXPer; ++k) {
-    const int e = tid + 256 * k;
-    rdst[k] = e < kXPieces ? xw_slot(e & 1, (e >> 1) / kXRC, (e >> 1) % kXRC) : -1;
-  }
-  // !UP2: the raw pieces straight from the input image, loaded 3 chunks ahead
-  // UP2: the block's 7 x 19 SOURCE pixels of a chunk into a 2-slot LDS buffer, loaded 4 chunks
-  //      ahead; each up-sampled piece of the raw region is then blended from its 4 source pixels
-  //      (krrn_bilerp4: the expression of the resize kernels, bit-identical) into the ring slot
-  constexpr int kLPer = UP2 ? kSPer : kXPer;
-  unsigned roff[kLPer], roffm[kLPer];  // roffm: the upper channel half masked (a last chunk of 4 channels)
-  int sdst[kLPer];                     // UP2: 16-B slot in a source buffer, -1: no piece
-  int upk[UP2 ? kXPer : 1];            // UP2: packed source slots of an up piece (-1: outside the image)
-  float uwy[UP2 ? kXPer : 1], uwx[UP2 ? kXPer : 1];
-  if constexpr (!UP2) {
-#pragma unroll
-    for (int k = 0; k < kXPer; ++k) {
-      const int e = tid + 256 * k;
-      const int pix = e >> 1, hh = e & 1;
-      const int rr = pix / kXRC, rc = pix - (pix / kXRC) * kXRC;
-      const int iy = 2 * ty0 - 1 + rr, ix = 2 * tx0 - 1 + rc;
-      const bool ok = e < kXPieces && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      roff[k] = ok ? (unsigned)((((long long)iy * a.W + ix) * a.in_cs + 4 * hh) * 4) : kWOOB;
-      roffm[k] = hh ? kWOOB : roff[k];
-      sdst[k] = -1;
-    }
-  } else {
-    int sy0, sx0, i1;
-    float l0, l1;
-    krrn_src_index(max(2 * ty0 - 1, 0), a.Hs, a.sh, 1, sy0, i1, l0, l1);
-    krrn_src_index(max(2 * tx0 - 1, 0), a.Ws, a.sw, 1, sx0, i1, l0, l1);
-#pragma unroll
-    for (int k = 0; k < kSPer; ++k) {
-      const int e = tid + 256 * k;
-      const int pix = e >> 1, hh = e & 1;
-      const int sr = pix / kSC, sc = pix - (pix / kSC) * kSC;
-      const int y = sy0 + sr, x = sx0 + sc;
-      const bool ok = e < kSPieces && y < a.Hs && x < a.Ws;
-      roff[k] = ok ? (unsigned)((((long long)y * a.Ws + x) * a.in_cs + 4 * hh) * 4) : kWOOB;
-      roffm[k] = hh ? kWOOB : roff[k];
-      sdst[k] = e < kSPieces ? e : -1;
-    }
-#pragma unroll
-    for (int k = 0; k < kXPer; ++k) {
-      const int e = tid + 256 * k;
-      const int pix = e >> 1, hh = e & 1;
-      const int rr = pix / kXRC, rc = pix - (pix / kXRC) * kXRC;
-      const int iy = 2 * ty0 - 1 + rr, ix = 2 * tx0 - 1 + rc;
-      int y0, y1, x0, x1;
-      float ly0, ly1, lx0, lx1;
-      krrn_src_index(max(iy, 0), a.Hs, a.sh, 1, y0, y1, ly0, ly1);
-      krrn_src_index(max(ix, 0), a.Ws, a.sw, 1, x0, x1, lx0, lx1);
-      const bool ok = e < kXPieces && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      const int i00 = ((y0 - sy0) * kSC + (x0 - sx0)) * 2 + hh;
-      upk[k] = ok ? (i00 | ((y1 - y0) * kSC * 2) << 12 | ((x1 - x0) * 2) << 20) : -1;
-      uwy[k] = ly1;
-      uwx[k] = lx1;
-    }
-  }
-  f32x4 raw[kLPer];
-  auto load_raw = [&](int ck) {  // chunks past the last reload the last (unused)
-    ck = min(ck, nck - 1);
-    const bool half = ck * kWC + 4 >= a.cin;
-#pragma unroll
-    for (int k = 0; k < kLPer; ++k)
-      raw[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, half ? roffm[k] : roff[k],
-                                                                              ck * kWC * 4, 0));
-  };
-  f32x4* const sbuf = reinterpret_cast<f32x4*>(smem) + 3 * kXSlot;  // UP2 source buffers [2][kSPieces]
-  auto store_raw = [&](int slot) {  // !UP2: ring slot; UP2: source buffer
-    if constexpr (!UP2) {
-      f32x4* dst = reinterpret_cast<f32x4*>(smem) + slot * kXSlot;
-#pragma unroll
-      for (int k = 0; k < kXPer; ++k)
-        if (rdst[k] >= 0) dst[rdst[k]] = raw[k];
-    } else {
-      f32x4* dst = sbuf + slot * kSPieces;
-#pragma unroll
-      for (int k = 0; k < kSPer; ++k)
-        if (sdst[k] >= 0) dst[sdst[k]] = raw[k];
-    }
-  };
-  auto upsample = [&](int sslot, int rslot) {  // UP2: source buffer -> ring slot
-    const f32x4* src = sbuf + sslot * kSPieces;
-    f32x4* dst = reinterpret_cast<f32x4*>(smem) + rslot * kXSlot;
-#pragma unroll
-    for (int k = 0; k < kXPer; ++k) {
-      if (rdst[k] < 0) continue;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (upk[k] >= 0) {
-        const int i00 = upk[k] & 0xfff, dy = (upk[k] >> 12) & 0xff, dx = upk[k] >> 20;
-        v = krrn_bilerp4(src[i00], src[i00 + dx], src[i00 + dy], src[i00 + dy + dx], 1.f - uwy[k], uwy[k],
-                         1.f - uwx[k], uwx[k]);
-      }
-      dst[rdst[k]] = v;
-    }
-  };
-
-  // split weights (plane U_mh b128 + plane U_l b64 per (chunk, xi, n, half)), two buffers
-  const int fr = lane & 31, h = lane >> 5;
-  const long long nrec = (long long)nck * 16 * a.N * 2;
-  const char* u3 = reinterpret_cast<const char*>(a.U);
-  const __amdgpu_buffer_rsrc_t rsMH =
-      __builtin_amdgcn_make_buffer_rsrc((void*)u3, (short)0, (int)min(nrec * 16, 0x7FFFFFFFLL), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsL =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(u3 + nrec * 16), (short)0, (int)min(nrec * 8, 0x7FFFFFFFLL), 0x00020000);
-  unsigned wrec[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) wrec[j] = (unsigned)(2 * min(n0 + 32 * j + fr, a.N - 1) + h);
-  u32x4 wmh[4][2];
-  u32x2 wl[4][2];
-  auto load_wv = [&](int ck, int v) {
-    ck = min(ck, nck - 1);
-    const unsigned srec = (unsigned)(((ck * 16 + 4 * wave + v) * a.N) * 2);  // uniform
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      wmh[v][j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsMH, wrec[j] * 16u, srec * 16u, 0));
-      wl[v][j] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsL, wrec[j] * 8u, srec * 8u, 0));
-    }
-  };
-
-  // this lane's patch rows of component row u = wave: t_u = d[ra] +- d[rb]; tile of M-block mb:
-  // (ty, tx) = (2 mb + fr / 16, fr % 16)
-  const int ra = wave == 0 ? 0 : (wave == 2 ? 2 : 1);
-  const int rb = wave == 0 ? 2 : (wave == 3 ? 3 : (wave == 1 ? 2 : 1));
-  const float sgn = wave == 1 ? 1.f : -1.f;
-  const int txl = fr & 15, tyl = fr >> 4;
-  int pa[2], pb[2];
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb) {
-    pa[mb] = xw_slot(h, 2 * (2 * mb + tyl) + ra, 2 * txl);
-    pb[mb] = xw_slot(h, 2 * (2 * mb + tyl) + rb, 2 * txl);
-  }
-
-  f32x16 acc[2][4][2];
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[mb][v][j][r] = 0.f;
-
-  // columns c = 0..3 of a patch row sit at slots p + (c & 1) * kXColP + (c >> 1)
-  auto make_v = [&](const f32x4* sl, int mb, f32x4 (&V)[4]) {
-    f32x4 t[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int co = (c & 1) * kXColP + (c >> 1);
-      const f32x4 da = sl[pa[mb] + co];
-      const f32x4 db = sl[pb[mb] + co];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) t[c][e] = __builtin_fmaf(sgn, db[e], da[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      V[0][e] = t[0][e] - t[2][e];
-      V[1][e] = t[1][e] + t[2][e];
-      V[2][e] = t[2][e] - t[1][e];
-      V[3][e] = t[1][e] - t[3][e];
-    }
-  };
-  // per chunk: both M-blocks' V (16 ds_read_b128), then per component v both M-blocks' MFMAs and
-  // the reload of v's weights for the next chunk (one weight buffer: 48 VGPRs)
-  auto chunk = [&](int ck) {
-    const f32x4* sl = reinterpret_cast<const f32x4*>(smem) + (ck % 3) * kXSlot;
-    f32x4 V[2][4];
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb) make_v(sl, mb, V[mb]);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb) {
-        const u32x8 ac = split3_chain(V[mb][v]);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const u32x8 bc = {wmh[v][j][0], wmh[v][j][1], wmh[v][j][2], wmh[v][j][3], wl[v][j][0], wl[v][j][1], 0u, 0u};
-          acc[mb][v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 2), acc[mb][v][j], 0, 0, 0);
-          acc[mb][v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 2), sub4(bc, 0), acc[mb][v][j], 0, 0, 0);
-          acc[mb][v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 4), sub4(bc, 0), acc[mb][v][j], 0, 0, 0);
-        }
-      }
-      load_wv(ck + 1, v);
-      // keep the reload here (hipcc otherwise sinks every weight load below all the MFMAs)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (!UP2) {
-      store_raw((ck + 2) % 3);
-      load_raw(ck + 3);
-    } else {
-      upsample((ck + 2) & 1, (ck + 2) % 3);
-      store_raw((ck + 3) & 1);
-      load_raw(ck + 4);
-    }
-    __syncthreads();
-  };
-
-  load_raw(0);
-#pragma unroll
-  for (int v = 0; v < 4; ++v) load_wv(0, v);
-  if constexpr (!UP2) {
-    store_raw(0);
-    load_raw(1);
-    __syncthreads();
-    store_raw(1);
-    load_raw(2);
-    __syncthreads();
-  } else {
-    // source chunk c sits in buffer c & 1; up-sampled chunk c in ring slot c % 3
-    store_raw(0);
-    load_raw(1);
-    __syncthreads();
-    upsample(0, 0);
-    store_raw(1);
-    load_raw(2);
-    __syncthreads();
-    upsample(1, 1);
-    store_raw(0);
-    load_raw(3);
-    __syncthreads();
-  }
-  for (int ck = 0; ck < nck; ++ck) chunk(ck);
-
-  // epilogue: (c0, c1) = (M[u][0] + M[u][1] + M[u][2], M[u][1] - M[u][2] - M[u][3]) of every (tile,
-  // channel) into LDS [u][q][tile][n], then each thread finishes 4 (tile, 4-channel) pairs
-#pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float m0 = acc[mb][0][j][r], m1 = acc[mb][1][j][r], m2 = acc[mb][2][j][r], m3 = acc[mb][3][j][r];
-        smem[((wave * 2 + 0) * kXT + row) * kXSP + j * 32 + fr] = m0 + m1 + m2;
-        smem[((wave * 2 + 1) * kXT + row) * kXSP + j * 32 + fr] = m1 - m2 - m3;
-      }
-  __syncthreads();
-  constexpr int kNP = kXT * kN4 / 256;
-#pragma unroll
-  for (int i = 0; i < kNP; ++i) {
-    const int pr = tid + 256 * i;
-    const int n4 = pr % kN4, tl = pr / kN4;
-    const int n = n0 + 4 * n4;
-    const int ty = ty0 + tl / kXGX, tx = tx0 + tl % kXGX;
-    if (ty >= a.Ht || tx >= a.Wt || n >= a.n_store) continue;
-    f32x4 c[4][2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) c[u][q] = *reinterpret_cast<const f32x4*>(smem + ((u * 2 + q) * kXT + tl) * kXSP + 4 * n4);
-    f32x4 y[4];
-    y[0] = c[0][0] + c[1][0] + c[2][0];
-    y[1] = c[0][1] + c[1][1] + c[2][1];
-    y[2] = c[1][0] - c[2][0] - c[3][0];
-    y[3] = c[1][1] - c[2][1] - c[3][1];
-    f32x4 scl = {1.f, 1.f, 1.f, 1.f}, bia = {0.f, 0.f, 0.f, 0.f};
-    if (a.vec) {
-      if (a.scale) scl = *reinterpret_cast<const f32x4*>(a.scale + n);
-      if (a.bias) bia = *reinterpret_cast<const f32x4*>(a.bias + n);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-      if (oy >= a.H || ox >= a.W) continue;
-      const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
-      if (a.vec) {
-        f32x4 v = y[q] * scl + bia;
-        if (a.res) v += *reinterpret_cast<const f32x4*>(a.res + pix * a.res_cs + a.res_co + n);
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        *reinterpret_cast<f32x4*>(a.out + pix * a.out_cs + a.out_co + n) = v;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (n + e >= a.n_store) break;
-          float v = y[q][e] * (a.scale ? a.scale[n + e] : 1.f) + (a.bias ? a.bias[n + e] : 0.f);
-          if (a.res) v += a.res[pix * a.res_cs + a.res_co + n + e];
-          if (a.relu) v = fmaxf(v, 0.f);
-          a.out[pix * a.out_cs + a.out_co + n + e] = v;
-        }
-      }
-    }
-  }
-}
-
 }  // namespace
-
-// split-bf16 kernel choice (krrn_wino_x3_variant): 0 = the 32-tile two-waves-per-SIMD kernel,
-// 1 = the 64-tile one-wave-per-SIMD kernel (wino_f23_x3w_kernel); env KRRN_WINO_X3W sets the start value
-static int g_wino_x3_variant = [] {
-  const char* e = getenv("KRRN_WINO_X3W");
-  return e ? atoi(e) : 0;
-}();
-
-KRRN_API int krrn_wino_x3_variant(int v) {
-  if (v < 0 || v > 1) return KRRN_EARG;
-  g_wino_x3_variant = v;
-  return KRRN_OK;
-}
 
 KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
                                    const float* U, int N, int n_store, const float* scale, const float* bias,
@@ -948,48 +577,8 @@ KRRN_API int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int
   // 32-bit buffer offsets: one image, and the U_hm plane (records x 16 B)
   const long long nrec = (long long)krrn_cdiv(cin, kWC) * 16 * N * 2;
   if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
-  if (g_wino_x3_variant == 1) {
-    const long long rbw = (long long)B * krrn_cdiv(a.Ht, kXGY) * krrn_cdiv(a.Wt, kXGX) * krrn_cdiv(N, kWN);
-    if (rbw > 0x7fffffffLL) return KRRN_ESHAPE;
-    hipLaunchKernelGGL(wino_f23_x3w_kernel<false>, dim3((unsigned)rbw), dim3(256), 0, (hipStream_t)stream, a);
-    return krrn_launch_status();
-  }
   const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kWN);
   if (rb > 0x7fffffffLL) return KRRN_ESHAPE;
   hipLaunchKernelGGL(wino_f23_x3_kernel, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
-  return krrn_launch_status();
-}
-
-KRRN_API int krrn_conv3x3_wino_x3_up2_f32(const float* in, int in_cs, int in_co, int B, int Hs, int Ws, int cin,
-                                          const void* U3, int N, int n_store, const float* scale, const float* bias,
-                                          const float* res, int res_cs, int res_co, float* out, int out_cs, int out_co,
-                                          int relu, void* stream) {
-  if (!in || !U3 || !out) return KRRN_EARG;
-  if (B < 1 || Hs < 2 || Ws < 2 || N < 1 || n_store < 1 || n_store > N) return KRRN_ESHAPE;
-  if (cin < 4 || (cin & 3) || (in_cs & 3) || (in_co & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
-  if (!krrn_aligned16(U3) || !krrn_aligned16(in)) return KRRN_EALIGN;
-  if (out_co + n_store > out_cs) return KRRN_ESHAPE;
-  WinoArgs a;
-  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = 2 * Hs; a.W = 2 * Ws; a.cin = cin;
-  a.Hs = Hs; a.Ws = Ws;
-  a.sh = (float)(Hs - 1) / (float)(2 * Hs - 1);  // align_corners=True (krrn_resize_bilinear_f32's scale)
-  a.sw = (float)(Ws - 1) / (float)(2 * Ws - 1);
-  a.img = (long long)Hs * Ws * in_cs;
-  a.U = reinterpret_cast<const float*>(U3); a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
-  a.res = res; a.res_cs = res_cs; a.res_co = res_co;
-  a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.relu = relu;
-  a.Ht = Hs; a.Wt = Ws;
-  const bool ov = !(out_cs & 3) && !(out_co & 3) && krrn_aligned16(out);
-  const bool rv = !res || (!(res_cs & 3) && !(res_co & 3) && krrn_aligned16(res));
-  const bool sv = (!scale || krrn_aligned16(scale)) && (!bias || krrn_aligned16(bias));
-  a.vec = (ov && rv && sv && !(n_store & 3)) ? 1 : 0;
-  const long long T = (long long)B * a.Ht * a.Wt;
-  if (T > 0x7fffffffLL) return KRRN_ESHAPE;
-  a.T = (int)T;
-  const long long nrec = (long long)krrn_cdiv(cin, kWC) * 16 * N * 2;
-  if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
-  const long long rbw = (long long)B * krrn_cdiv(a.Ht, kXGY) * krrn_cdiv(a.Wt, kXGX) * krrn_cdiv(N, kWN);
-  if (rbw > 0x7fffffffLL) return KRRN_ESHAPE;
-  hipLaunchKernelGGL(wino_f23_x3w_kernel<true>, dim3((unsigned)rbw), dim3(256), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }

@@ -50,11 +50,6 @@ GEMM_1X1 = os.environ.get("KRRN_GEMM_1X1", "1") == "1"
 FUSE_ID_FIRST = os.environ.get("KRRN_FUSE_ID_FIRST", "1") == "1"
 # Winograd convs on the bf16 matrix cores with f32-accurate split operands (krrn_conv3x3_wino_x3_f32)
 WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
-# the heads' x2 upsample + 3x3 conv as one launch (krrn_conv3x3_wino_x3_up2_f32: the upsample is
-# blended while the Winograd input is staged, never written). Off by default: the blend adds ~13 % of
-# VALU to an issue-bound kernel, about what the resize's 472 MB write + re-read costs (step medians
-# 5427 vs 5499 crops/s, three alternating runs on one box)
-UP2_FUSE = os.environ.get("KRRN_UP2_FUSE", "0") == "1"
 # implicit-GEMM convs (transposed convs, stem / transitions) likewise (krrn_conv2d[_group]_x3_f32)
 CONV_X3 = os.environ.get("KRRN_CONV_X3", "1") == "1"
 
@@ -248,24 +243,10 @@ class _Builder:
         return out
 
     def conv_up2(self, x: Act, conv: nn.Module, bn: Optional[nn.Module], relu: bool = False) -> Act:
-        """conv(UpsamplingBilinear2d(scale 2)(x)) (krrn.py:56-58, 78-80): one fused launch when the conv
-        runs on the split Winograd kernel, else the upsample materialised (resize) and the conv."""
-        spec = ops.make_conv(conv, bn, self.dev, cin_p=x.cp)
+        """conv(UpsamplingBilinear2d(scale 2)(x)) (krrn.py:56-58, 78-80): the upsample materialised
+        (resize) and the conv. Blending the upsample into the split Winograd's input staging instead
+        was measured slower and removed."""
         H, W = 2 * x.H, 2 * x.W
-        if (UP2_FUSE and WINO_X3 and ops.wino_eligible(spec, x.B * H * W) and x.cs % 4 == 0 and x.co % 4 == 0
-                and x.H >= 2 and x.W >= 2):
-            self.specs.append(spec)
-            out = self.act(H, W, spec.cout)
-            U = ops.wino_weights_x3(ops.wino_weights(conv, self.dev, cin_p=x.cp))
-            self.specs.append(U)
-            np_ = pad4(spec.cout)
-            M = x.B * H * W
-            pipe = 2.0 * 16 * spec.cin_p * np_ * x.B * x.H * x.W
-            self.plan.add("krrn_conv3x3_wino_x3_up2_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(U), np_,
-                          np_, ptr(spec.scale), ptr(spec.bias), ptr(None), 0, 0, ptr(out.t), out.cs, out.co, int(relu),
-                          meta=dict(kernel="wino_f23_x3", flops=2.0 * spec.cin * spec.cout * 9 * M, tag="conv_up2_wino",
-                                    M=M, N=np_, K=spec.cin_p * 9, mfma_flops=pipe * 6 / 16, mfma_bf16_flops=pipe * 6))
-            return out
         up = self.act(H, W, x.c)
         self.resize(x, up, align=True)
         return self.conv(up, conv, bn, relu=relu)

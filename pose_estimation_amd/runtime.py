@@ -49,8 +49,6 @@ _lib.register("krrn_conv2d_group_x3_f32", [P, I, I, P])
 _lib.register("krrn_conv2d_x3_f32", [P, I, I, I, I, I, I, I, I, I, I, P, P, P, I, I, P, P, P, I, P, I, I, P, I, I, I, I,
                                      I, I, I, I, I, I, I, P, P])
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
-_lib.register("krrn_wino_x3_variant", [I])
-_lib.register("krrn_conv3x3_wino_x3_up2_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv3x3_wino_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv1x1_nchw_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
 _lib.register("krrn_conv1x1_nchw_x3_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])

@@ -1,5 +1,4 @@
 """Implicit-GEMM conv kernel vs a plain PyTorch fp32 reference of the same op."""
-import os
 
 import pytest
 import torch
@@ -297,73 +296,17 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     torch.testing.assert_close(got, ref, **TOL)
     assert torch.count_nonzero(out.t[..., np_:]).item() == 0
     U3 = ops.wino_weights_x3(U)
-    outs3 = []
-    try:
-        for variant in (0, 1):  # 32-tile two-waves-per-SIMD, 64-tile one-wave-per-SIMD
-            _lib.check(L.krrn_wino_x3_variant(variant), "krrn_wino_x3_variant")
-            out.t.fill_(float("nan"))
-            out.t[..., np_:] = 0.0
-            _lib.check(L.krrn_conv3x3_wino_x3_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_, np_,
-                                                  ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
-                                                  out.cs, 0, 1, P(torch.cuda.current_stream().cuda_stream)), "wino_x3")
-            torch.cuda.synchronize()
-            outs3.append(out.t.clone())
-    finally:
-        L.krrn_wino_x3_variant(int(os.environ.get("KRRN_WINO_X3W", "0")))
-    # the two split kernels: the same V / U operands and per-accumulator MFMA order, bit-identical
-    assert torch.equal(outs3[0], outs3[1])
-    got3 = outs3[0][..., :cout].permute(0, 3, 1, 2).cpu()
+    out.t.fill_(float("nan"))
+    out.t[..., np_:] = 0.0
+    _lib.check(L.krrn_conv3x3_wino_x3_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_, np_,
+                                          ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t),
+                                          out.cs, 0, 1, P(torch.cuda.current_stream().cuda_stream)), "wino_x3")
+    torch.cuda.synchronize()
+    got3 = out.t[..., :cout].permute(0, 3, 1, 2).cpu()
     torch.testing.assert_close(got3, ref, **TOL)
-    assert torch.count_nonzero(outs3[0][..., np_:]).item() == 0
+    assert torch.count_nonzero(out.t[..., np_:]).item() == 0
     scale = float(ref.abs().max())
     torch.testing.assert_close(got3, got, rtol=1e-5, atol=2e-6 * scale)
-
-
-@pytest.mark.parametrize("B,cin,cout,Hs,Ws,co", [(3, 128, 128, 30, 30, 0), (2, 64, 72, 17, 23, 4), (2, 36, 40, 5, 9, 0),
-                                                  (2, 132, 64, 8, 40, 0)])
-def test_conv3x3_wino_up2(dev, B, cin, cout, Hs, Ws, co):
-    """krrn_conv3x3_wino_x3_up2_f32 (the x2 align_corners upsample blended while the Winograd input is
-    staged) equals krrn_resize_bilinear_f32 + the same kernel on the materialised upsample bit for
-    bit, and torch's UpsamplingBilinear2d + conv + BN + ReLU at f32 tolerance (krrn.py:56-58)."""
-    from pose_estimation_amd import _lib
-    from pose_estimation_amd.runtime import P, ptr
-    g = torch.Generator().manual_seed(cin + cout + Hs)
-    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
-    with torch.no_grad():
-        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
-    bn = _bn(cout, g)
-    x = torch.randn(B, cin, Hs, Ws, generator=g)
-    up = nn.UpsamplingBilinear2d(scale_factor=2.0)(x)
-    ref = torch.relu(bn(conv(up))).detach()
-    H, W = 2 * Hs, 2 * Ws
-    cs = ops.pad4(cin) + co + 4
-    xa = _nhwc(x, dev, cs=cs, co=co)
-    spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
-    U3 = ops.wino_weights_x3(ops.wino_weights(conv, dev, cin_p=ops.pad4(cin)))
-    np_ = ops.pad4(cout)
-    L = _lib.lib()
-    st = P(torch.cuda.current_stream().cuda_stream)
-    fused = ops.new_act(B, H, W, cout, dev, cs=np_ + 4)
-    fused.t.fill_(float("nan"))
-    _lib.check(L.krrn_conv3x3_wino_x3_up2_f32(ptr(xa.t), xa.cs, xa.co, B, Hs, Ws, ops.pad4(cin), ptr(U3), np_, np_,
-                                              ptr(spec.scale), ptr(spec.bias), ptr(None), 0, 0, ptr(fused.t), fused.cs,
-                                              0, 1, st), "wino_up2")
-    upa = ops.new_act(B, H, W, ops.pad4(cin), dev, cs=ops.pad4(cin))
-    _lib.check(L.krrn_resize_bilinear_f32(ptr(xa.t), B, Hs, Ws, xa.cs, xa.co, ops.pad4(cin), ptr(upa.t), H, W, upa.cs,
-                                          0, ptr(None), 0, 0, 1, 0, st), "resize")
-    two = ops.new_act(B, H, W, cout, dev, cs=np_ + 4)
-    two.t.fill_(float("nan"))
-    try:
-        _lib.check(L.krrn_wino_x3_variant(1), "krrn_wino_x3_variant")
-        _lib.check(L.krrn_conv3x3_wino_x3_f32(ptr(upa.t), upa.cs, 0, B, H, W, ops.pad4(cin), ptr(U3), np_, np_,
-                                              ptr(spec.scale), ptr(spec.bias), ptr(None), 0, 0, ptr(two.t), two.cs, 0, 1,
-                                              st), "wino_x3")
-    finally:
-        L.krrn_wino_x3_variant(int(os.environ.get("KRRN_WINO_X3W", "0")))
-    torch.cuda.synchronize()
-    assert torch.equal(fused.t[..., :np_], two.t[..., :np_])
-    got = fused.t[..., :cout].permute(0, 3, 1, 2).cpu()
-    torch.testing.assert_close(got, ref, **TOL)
 
 
 @pytest.mark.parametrize("B,cin,cout,H,W,co,nw,ks,k,st", [
