@@ -18,7 +18,8 @@
 //     per 8 k take register slices, W[h l] x A[h h] = hh + lh, W[m h] x A[h m] = mh + hm,
 //     W[m h] x A[m l] = mm + hl; one barrier per tile, two blocks per CU (56 KB LDS, 2 waves per SIMD);
 //   * the previous tile's accumulator is stored in the current tile's MFMA gaps as 4 float4 per lane
-//     (operands swapped so a lane holds 4 consecutive columns), bias (from LDS) / residual / ReLU fused.
+//     (operands swapped so a lane holds 4 consecutive columns; transposed through LDS first so each
+//     store instruction writes whole 128-B row segments), bias (from LDS) / residual / ReLU fused.
 // The row panels of a launch split into `csplit` column ranges when the panels alone cannot fill
 // the chip (level 1: M = 16000 -> 125 panels x 4 column ranges).
 #include "krrn_common.h"
@@ -67,6 +68,17 @@ __device__ __forceinline__ gp_bf16x8 gp_sub4(const gp_u32x8& c, int o) {
 // that the DMA into one does not alias the reads of the other.
 typedef __attribute__((address_space(3))) void gp_lds_void;
 
+// Transposed stores (KRRN_PANEL_TSTORE, default on; the float4 epilogue only): a lane's accumulator is
+// 4 float4 of ONE row, so a direct store instruction writes 32 rows x 32 B; the tile instead goes
+// through a per-wave LDS slot and comes back as 8 lanes per row, and each store instruction writes 8
+// whole 128-B row segments. The stores are buffer stores through a per-wave resource bounded by the
+// wave's valid rows: rows past M are dropped by the hardware, so a live wave always issues its 4
+// stores per tile (the vmcnt(4) accounting below depends on it).
+#ifndef KRRN_PANEL_TSTORE
+#define KRRN_PANEL_TSTORE 1
+#endif
+constexpr int kTP = 36;  // LDS pitch of a transposed tile row (floats; conflict-free b128 writes)
+
 template <int KT, bool RES>
 __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g) {
   constexpr int G = KT / 8;
@@ -76,6 +88,9 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
   __shared__ __attribute__((aligned(16))) unsigned sbA[TILE_U32];
   __shared__ __attribute__((aligned(16))) unsigned sbB[TILE_U32];
   __shared__ float sbias[kPanelMaxN];
+#if KRRN_PANEL_TSTORE
+  __shared__ __attribute__((aligned(16))) float stile[4][32 * kTP];
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nl = lane & 31, fh = lane >> 5;
@@ -128,6 +143,34 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
   const float* rrow = RES ? g.res + (size_t)(m0 + mrow) * g.ldr : nullptr;
   const bool row_ok = mrow < rows_left;
   f32x4 rv[RES ? 4 : 1];
+#if KRRN_PANEL_TSTORE
+  float* const tw = stile[wave];
+  const int trow = lane >> 3, tcol = 4 * (lane & 7);  // store j: row 8 j + trow, columns tcol .. + 3
+  const int vrows = live ? min(32, rows_left) : 0;
+  const __amdgpu_buffer_rsrc_t rsO = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.out + (size_t)(live ? m0 : 0) * g.ldo), (short)0, vrows * g.ldo * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(RES && g.res ? g.res + (size_t)(live ? m0 : 0) * g.ldr : g.out), (short)0,
+      RES && g.res ? vrows * g.ldr * 4 : 0, 0x00020000);
+  f32x4 tv[4];
+  auto epilogue_t = [&](int ctp, int j) {
+    const int n = ctp * 32 + tcol;
+    f32x4 v = tv[j] + *reinterpret_cast<const f32x4*>(sbias + n);
+    if constexpr (RES) v += rv[j];
+    if (g.relu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    const unsigned vo = (unsigned)(((8 * j + trow) * g.ldo + tcol) * 4);
+    if (g.vec) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gp_u32x4, v), rsO, vo, ctp * 128, 0);
+    } else {  // out / ldo not 16-B aligned: four dword stores
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[e]), rsO, vo + 4 * e, ctp * 128, 0);
+    }
+  };
+#endif
   auto epilogue = [&](const f32x16& acc, int ctp, int q) {
     if (!row_ok) return;
     const int n = ctp * 32 + 8 * q + 4 * fh;
@@ -157,12 +200,40 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
   auto step = [&](int ct, const unsigned* cur, unsigned* nxt) {
     const bool has = ct < ct1;
     const bool st = live && ct > ct0;
+#if KRRN_PANEL_TSTORE
+    if (st) {
+      // tile ct - 1 through the wave's LDS slot: written as (row nl, columns 8 q + 4 fh), read back as
+      // (row 8 j + trow, columns tcol); the slot is this wave's alone and a wave's LDS accesses stay in order
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(tw + nl * kTP + 8 * q + 4 * fh) =
+            f32x4{accp[4 * q], accp[4 * q + 1], accp[4 * q + 2], accp[4 * q + 3]};
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tv[j] = *reinterpret_cast<const f32x4*>(tw + (8 * j + trow) * kTP + tcol);
+      __builtin_amdgcn_wave_barrier();
+      if constexpr (RES) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned ro = (unsigned)(((8 * j + trow) * g.ldr + tcol) * 4);
+          if (g.vec) {
+            rv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, ro, (ct - 1) * 128, 0));
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              rv[j][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsR, ro + 4 * e, (ct - 1) * 128, 0));
+          }
+        }
+      }
+    }
+#else
     if constexpr (RES) {
       if (g.vec && st && row_ok) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) rv[q] = *reinterpret_cast<const f32x4*>(rrow + (ct - 1) * 32 + 8 * q + 4 * fh);
       }
     }
+#endif
     if (ct + 1 < ct1) dma_tile(ct + 1, nxt);  // its last readers (tile ct - 1) passed the previous barrier
     f32x16 acc;
 #pragma unroll
@@ -178,7 +249,11 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(mh), gp_sub4(ca[gi], 2), acc, 0, 0, 0);  // mh + hm
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(mh), gp_sub4(ca[gi], 4), acc, 0, 0, 0);  // mm + hl
       }
+#if KRRN_PANEL_TSTORE
+      if (st && gi % (G / 4) == 0) epilogue_t(ct - 1, gi / (G / 4));
+#else
       if (st && gi % (G / 4) == 0) epilogue(accp, ct - 1, gi / (G / 4));
+#endif
     }
     accp = acc;
     // this wave's DMA into nxt must have landed before any wave reads it: vmcnt retires in order and

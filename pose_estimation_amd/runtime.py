@@ -488,10 +488,20 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
             and a_off % 4 == 0 and not (K == 128 and res is not None):
         wp = ops.gemm_weights_panel(w)
         plan.buffers.append([wp, bias])
-        rows = (M + 255) // 256  # 256-row blocks, one per CU (96 KB of LDS each)
         csplit = 1
-        while rows * csplit < 256 and (N // 32) % (2 * csplit) == 0:  # fill the chip: >= 256 blocks
-            csplit *= 2
+        tiles = N // 32
+        if K == 128:
+            # the level-0 / level-1 GCN GEMMs (128-row blocks, two per CU): about 16 column tiles per
+            # block and at least 512 blocks; measured (profiles/bench_fusion_kernels.py, round 4) level 0
+            # (M = 64000) 124 us at csplit 2 against 132 at 1, level 1 (M = 16000) 35 us at 4 against 42 at 8
+            blocks = (M + 127) // 128
+            while tiles % (2 * csplit) == 0 and (tiles // csplit > 16 or
+                                                 (blocks * csplit < 512 and tiles // csplit >= 16)):
+                csplit *= 2
+        else:
+            rows = (M + 255) // 256
+            while rows * csplit < 256 and tiles % (2 * csplit) == 0:  # fill the chip: >= 256 blocks
+                csplit *= 2
         plan.add("krrn_gemm_panel_x3_f32", P(a.data_ptr() + 4 * a_off), lda, M, K, N, ptr(wp), ptr(bias), ptr(res),
                  ldr, ptr(out), ldo, int(relu), csplit,
                  meta=dict(kernel="gemm_panel_x3", flops=flops, tag=tag, M=M, N=N, K=K, splits=csplit,
