@@ -267,6 +267,17 @@ static void pinv3(const double* a, double* r) {
  * The rows of M^T M in SUM_WAVE: group g = lane / 16 sums points g, g + 4, ... in order, then
  * (G0 + G1) + (G2 + G3). */
 enum { SUM_SEQ = 0, SUM_WAVE = 1 };
+/* diagnostics of the last EPnP call (oracle_pnp_hypotheses_diag): the winning approximation
+ * (1..3) and whether its Procrustes hit det(U V^T) < 0 (Kabsch: diag(1,1,-1); OpenCV: third row
+ * negated) */
+static int g_diag_approx, g_diag_detneg[4];
+/* diagnostics only (tests/pnp_divergence.py), 0 everywhere else: swaps single ingredients of the
+ * OpenCV-semantics EPnP for the kernel's -- bit 0: the 12 x 12 null-space basis from the kernel's
+ * parallel-ordered Jacobi; bit 1: the kernel's Procrustes (U from the cross-product frame) instead of
+ * the SVD one; bit 2: the beta and Gauss-Newton solves by the kernel's Cholesky normal equations;
+ * bit 3: the kernel's Procrustes without the det rule (plain Kabsch, the kernel before round 5) */
+static int g_cv_variant;
+void oracle_set_cv_variant(int v) { g_cv_variant = v; }
 static double contrib_buf[MAXP * 12];
 
 /* out[k] = sum over points of contrib[p * nv + k], in the kernel's order */
@@ -289,7 +300,9 @@ static void reduce_points(int mode, int n, int nv, const double* contrib, double
   }
 }
 
-/* Kabsch on the 3x3 correlation H (csrc/pnp.hip kabsch): R = U diag(1,1,det) V^T. */
+/* Procrustes on the 3x3 correlation H as csrc/pnp.hip kabsch evaluates it, with OpenCV's epnp.cpp
+ * rule: R = U V^T, third row negated when det < 0 (for a rank-3 H: Kabsch's U diag(1,1,-1) V^T with
+ * the third row negated); a rank-deficient H (coplanar points) keeps the proper Kabsch rotation. */
 static void kabsch(const double* H, double* R) {
   /* SVD H = U S V^T through eig(H^T H) = V S^2 V^T, U = H V / S */
   double HtH[9], w[3], V[9];
@@ -321,10 +334,17 @@ static void kabsch(const double* H, double* R) {
   U[8] = U[0] * U[4] - U[1] * U[3];
   /* third right vector consistent with det(V) = +1 */
   double v2[3] = {V[1] * V[5] - V[2] * V[4], V[2] * V[3] - V[0] * V[5], V[0] * V[4] - V[1] * V[3]};
-  /* R = sum_i u_i v_i^T (u2 = u0 x u1, v2 = v0 x v1 gives det(R) = +1: Kabsch) */
+  const double detH = H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) +
+                      H[2] * (H[3] * H[7] - H[4] * H[6]);
+  const int refl = (g_cv_variant & 8) ? 0 : (detH < 0.0 && w[2] > 1e-24 * w[0]);
+  const double s2 = refl ? -1.0 : 1.0;
+  /* R = sum_i u_i v_i^T (u2 = u0 x u1, v2 = v0 x v1: det(R) = +1, Kabsch), u2 negated for a reflection */
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 3; ++c)
-      R[r * 3 + c] = U[0 * 3 + r] * V[0 * 3 + c] + U[1 * 3 + r] * V[1 * 3 + c] + U[2 * 3 + r] * v2[c];
+      R[r * 3 + c] = U[0 * 3 + r] * V[0 * 3 + c] + U[1 * 3 + r] * V[1 * 3 + c] + (s2 * U[2 * 3 + r]) * v2[c];
+  if (refl) {
+    R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8];
+  }
 }
 
 /* ---------------- EPnP ---------------- */
@@ -422,6 +442,8 @@ static double r_and_t(int mode, const double* ut, const double betas[4], const d
       for (int c = 0; c < 3; ++c) contrib_buf[9 * p + 3 * r + c] = (pc[r] - cc[r]) * (pw[3 * p + c] - cw[c]);
   }
   reduce_points(mode, n, 9, contrib_buf, H);
+  g_diag_detneg[0] = (H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) +
+                      H[2] * (H[3] * H[7] - H[4] * H[6])) < 0;
   kabsch(H, R);
   for (int r = 0; r < 3; ++r) t[r] = cc[r] - (R[r * 3 + 0] * cw[0] + R[r * 3 + 1] * cw[1] + R[r * 3 + 2] * cw[2]);
   for (int p = 0; p < n; ++p) {
@@ -518,6 +540,7 @@ static double epnp_mode(int mode, const double* pw, const double* uv, int n, Cam
     }
     gauss_newton(L, rho, betas);
     errs[1] = r_and_t(mode, ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[1], ts[1]);
+    g_diag_detneg[1] = g_diag_detneg[0];
   }
   /* approx 2: B11 B12 B22 from columns 0 1 2 */
   {
@@ -537,6 +560,7 @@ static double epnp_mode(int mode, const double* pw, const double* uv, int n, Cam
     betas[3] = 0.0;
     gauss_newton(L, rho, betas);
     errs[2] = r_and_t(mode, ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[2], ts[2]);
+    g_diag_detneg[2] = g_diag_detneg[0];
   }
   /* approx 3: B11 B12 B22 B13 B23 from columns 0..4 */
   {
@@ -556,10 +580,12 @@ static double epnp_mode(int mode, const double* pw, const double* uv, int n, Cam
     betas[3] = 0.0;
     gauss_newton(L, rho, betas);
     errs[3] = r_and_t(mode, ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[3], ts[3]);
+    g_diag_detneg[3] = g_diag_detneg[0];
   }
   int N = 1;
   if (errs[2] < errs[1]) N = 2;
   if (errs[3] < errs[N]) N = 3;
+  g_diag_approx = N;
   memcpy(R, Rs[N], sizeof(double) * 9);
   memcpy(t, ts[N], sizeof(double) * 3);
   return errs[N];
@@ -771,7 +797,8 @@ static void gauss_newton_cv(const double* L, const double* rho, double betas[4])
                        l[6] * betas[0] * betas[3] + l[7] * betas[1] * betas[3] + l[8] * betas[2] * betas[3] +
                        l[9] * betas[3] * betas[3]);
     }
-    qr_solve6x4(A, b, x);
+    if (g_cv_variant & 4) lsq_solve(A, 6, 4, b, x);
+    else qr_solve6x4(A, b, x);
     for (int k = 0; k < 4; ++k) betas[k] += x[k];
   }
 }
@@ -808,25 +835,27 @@ static double r_and_t_cv(const double* ut, const double betas[4], const double* 
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) AtA[3 * i + j] = ABt[i] * ABt[j] + ABt[3 + i] * ABt[3 + j] + ABt[6 + i] * ABt[6 + j];
   jacobi_eig(AtA, 3, w, V);
-  for (int i = 0; i < 3; ++i) {
-    double u[3];
-    for (int r = 0; r < 3; ++r) u[r] = ABt[3 * r] * V[3 * i] + ABt[3 * r + 1] * V[3 * i + 1] + ABt[3 * r + 2] * V[3 * i + 2];
-    double nr = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-    if (i == 2 && nr < 1e-12 * sqrt(fmax(w[0], 0.0))) { /* rank 2: complete the left frame */
-      u[0] = U[1] * U[5] - U[2] * U[4];
-      u[1] = U[2] * U[3] - U[0] * U[5];
-      u[2] = U[0] * U[4] - U[1] * U[3];
-      nr = 1.0;
+  if (!(w[2] > 1e-24 * w[0]) || (g_cv_variant & 2)) {
+    /* rank-deficient H (coplanar points): the third singular pair and so the sign of det(U V^T) are
+     * the SVD's arbitrary choice; the proper rotation (Kabsch) is taken, as csrc/pnp.hip does */
+    g_diag_detneg[0] = 0;
+    kabsch(ABt, R);
+  } else {
+    for (int i = 0; i < 3; ++i) {
+      double u[3];
+      for (int r = 0; r < 3; ++r) u[r] = ABt[3 * r] * V[3 * i] + ABt[3 * r + 1] * V[3 * i + 1] + ABt[3 * r + 2] * V[3 * i + 2];
+      double nr = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+      if (nr < 1e-300) nr = 1e-300;
+      for (int r = 0; r < 3; ++r) U[3 * i + r] = u[r] / nr;
     }
-    if (nr < 1e-300) nr = 1e-300;
-    for (int r = 0; r < 3; ++r) U[3 * i + r] = u[r] / nr;
-  }
-  for (int r = 0; r < 3; ++r)
-    for (int c = 0; c < 3; ++c) R[3 * r + c] = U[r] * V[c] + U[3 + r] * V[3 + c] + U[6 + r] * V[6 + c];
-  const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
-                     R[2] * (R[3] * R[7] - R[4] * R[6]);
-  if (det < 0) {
-    R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) R[3 * r + c] = U[r] * V[c] + U[3 + r] * V[3 + c] + U[6 + r] * V[6 + c];
+    const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                       R[2] * (R[3] * R[7] - R[4] * R[6]);
+    g_diag_detneg[0] = det < 0;
+    if (det < 0) {
+      R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8];
+    }
   }
   for (int r = 0; r < 3; ++r) t[r] = cc[r] - (R[3 * r] * cw[0] + R[3 * r + 1] * cw[1] + R[3 * r + 2] * cw[2]);
   double err = 0.0;
@@ -859,7 +888,14 @@ static double epnp_cv(const double* pw, const double* uv, int n, Cam cam, double
       for (int j = 0; j < 12; ++j) MtM[i * 12 + j] += r1[i] * r1[j] + r2[i] * r2[j];
   }
   double w[12], ut[144];
-  jacobi_eig(MtM, 12, w, ut); /* rows of ut: eigenvectors, descending: rows 11..8 = the 4 smallest */
+  if (g_cv_variant & 1) {
+    double v4[4][12];
+    jacobi12_par(MtM, v4);
+    for (int q = 0; q < 4; ++q)
+      for (int k = 0; k < 12; ++k) ut[(11 - q) * 12 + k] = v4[q][k];
+  } else {
+    jacobi_eig(MtM, 12, w, ut); /* rows of ut: eigenvectors, descending: rows 11..8 = the 4 smallest */
+  }
   double L[60], rho[6];
   {
     const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
@@ -898,7 +934,8 @@ static double epnp_cv(const double* pw, const double* uv, int n, Cam cam, double
     double A[30], x[5];
     for (int i = 0; i < 6; ++i)
       for (int j = 0; j < nb; ++j) A[nb * i + j] = L[10 * i + (approx == 1 ? cols1[j] : j)];
-    lsq_svd(A, 6, nb, rho, x);
+    if (g_cv_variant & 4) lsq_solve(A, 6, nb, rho, x);
+    else lsq_svd(A, 6, nb, rho, x);
     if (approx == 1) {
       if (x[0] < 0) {
         betas[0] = sqrt(-x[0]);
@@ -921,10 +958,12 @@ static double epnp_cv(const double* pw, const double* uv, int n, Cam cam, double
     }
     gauss_newton_cv(L, rho, betas);
     errs[approx] = r_and_t_cv(ut, betas, pw, uv, n, cws, ci, cw, cam, Rs[approx], ts[approx]);
+    g_diag_detneg[approx] = g_diag_detneg[0];
   }
   int N = 1;
   if (errs[2] < errs[1]) N = 2;
   if (errs[3] < errs[N]) N = 3;
+  g_diag_approx = N;
   memcpy(R, Rs[N], sizeof(double) * 9);
   memcpy(t, ts[N], sizeof(double) * 3);
   return errs[N];
@@ -996,4 +1035,48 @@ int oracle_pnp_ransac_cv(const float* obj, const float* img, int P, const float*
   memcpy(R_out, bR, sizeof bR);
   memcpy(t_out, bt, sizeof bt);
   return best >= 0 ? best_cnt : 0;
+}
+
+/* Diagnostics (tests/pnp_divergence.py): every hypothesis under either numerics (cv = 0: the
+ * kernel-order EPnP, 1: the OpenCV-semantics one) -> f32 pose, inlier count, and per hypothesis
+ * diag = approx (1..3) + 4 * (its Procrustes had det < 0) + 8 * (any approximation's did). */
+void oracle_pnp_hypotheses_diag(const float* obj, const float* img, int P, const float* K4, const int* subsets,
+                                int H, float thr, int cv, float* R_out, float* t_out, int* cnt_out, int* diag) {
+  Cam cam = {K4[0], K4[1], K4[2], K4[3]};
+  const float thr2 = thr * thr;
+  for (int h = 0; h < H; ++h) {
+    double spw[15], suv[10], R[9], t[3];
+    for (int i = 0; i < 5; ++i) {
+      const int id = subsets[5 * h + i];
+      for (int k = 0; k < 3; ++k) spw[3 * i + k] = obj[3 * id + k];
+      for (int k = 0; k < 2; ++k) suv[2 * i + k] = img[2 * id + k];
+    }
+    if (cv) epnp_cv(spw, suv, 5, cam, R, t);
+    else epnp(spw, suv, 5, cam, R, t);
+    float Rf[9], tf[3];
+    for (int i = 0; i < 9; ++i) Rf[i] = (float)R[i];
+    for (int i = 0; i < 3; ++i) tf[i] = (float)t[i];
+    int cnt = 0;
+    for (int p = 0; p < P; ++p) {
+      const float X = obj[3 * p], Y = obj[3 * p + 1], Z = obj[3 * p + 2];
+      const float xc = Rf[0] * X + Rf[1] * Y + Rf[2] * Z + tf[0];
+      const float yc = Rf[3] * X + Rf[4] * Y + Rf[5] * Z + tf[1];
+      const float zc = Rf[6] * X + Rf[7] * Y + Rf[8] * Z + tf[2];
+      float du, dv;
+      if (cv) {
+        du = img[2 * p] - ((float)cam.fu * xc / zc + (float)cam.uc);
+        dv = img[2 * p + 1] - ((float)cam.fv * yc / zc + (float)cam.vc);
+      } else {
+        const float iz = 1.0f / zc;
+        du = img[2 * p] - ((float)cam.fu * xc * iz + (float)cam.uc);
+        dv = img[2 * p + 1] - ((float)cam.fv * yc * iz + (float)cam.vc);
+      }
+      if (du * du + dv * dv <= thr2) ++cnt;
+    }
+    memcpy(R_out + 9 * h, Rf, sizeof Rf);
+    memcpy(t_out + 3 * h, tf, sizeof tf);
+    cnt_out[h] = cnt;
+    diag[h] = g_diag_approx + 4 * g_diag_detneg[g_diag_approx] +
+              8 * (g_diag_detneg[1] | g_diag_detneg[2] | g_diag_detneg[3]);
+  }
 }

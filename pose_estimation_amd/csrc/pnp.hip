@@ -551,7 +551,12 @@ __device__ __forceinline__ void gauss_newton(const double (&Lr)[10], double rho_
   }
 }
 
-// Kabsch on the 3x3 correlation H = sum (pc - cc)(pw - cw)^T: R = U diag(1,1,det) V^T.
+// Procrustes on the 3x3 correlation H = sum (pc - cc)(pw - cw)^T as OpenCV's epnp.cpp
+// estimate_R_and_t does it: R = U V^T of H's SVD, and when det(R) < 0 its third row negated. For a
+// rank-3 H, U V^T is the polar factor (det = sign det H), which is the Kabsch rotation
+// U diag(1,1,1) V^T when det H > 0 and U diag(1,1,-1) V^T otherwise (u2 = u0 x u1, v2 = v0 x v1 below).
+// A rank-deficient H (coplanar points) leaves cv2's result to its SVD's sign choices; it is kept
+// proper (Kabsch) here. oracle/pnp_ref.c restates it (kabsch).
 __device__ __forceinline__ void kabsch(const double (&H)[9], double (&R)[9]) {
   double HtH[9], w[3], V[9];
 #pragma unroll
@@ -583,10 +588,17 @@ __device__ __forceinline__ void kabsch(const double (&H)[9], double (&R)[9]) {
   U[7] = U[2] * U[3] - U[0] * U[5];
   U[8] = U[0] * U[4] - U[1] * U[3];
   const double v2[3] = {V[1] * V[5] - V[2] * V[4], V[2] * V[3] - V[0] * V[5], V[0] * V[4] - V[1] * V[3]};
+  const double detH = H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) +
+                      H[2] * (H[3] * H[7] - H[4] * H[6]);
+  const bool refl = detH < 0.0 && w[2] > 1e-24 * w[0];
+  const double s2 = refl ? -1.0 : 1.0;
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) R[r * 3 + c] = U[r] * V[c] + U[3 + r] * V[3 + c] + U[6 + r] * v2[c];
+    for (int c = 0; c < 3; ++c) R[r * 3 + c] = U[r] * V[c] + U[3 + r] * V[3 + c] + (s2 * U[6 + r]) * v2[c];
+  if (refl) {
+    R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8];
+  }
 }
 
 // R, t from betas (lane r holds component r of the 4 null-space vectors: vq); returns the mean

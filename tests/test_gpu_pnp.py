@@ -213,38 +213,96 @@ def test_full_ransac_matches_oracle(dev, noise_px, outliers):
     assert worst < 1e-6, worst
 
 
-@pytest.mark.parametrize("noise_px,pose_tol", [(0.0, 1e-4), (0.4, 1e-2)])
-def test_ransac_matches_opencv_semantics_oracle(dev, noise_px, pose_tol):
+@pytest.mark.parametrize("noise_px", [0.0, 0.4])
+def test_ransac_matches_opencv_semantics_oracle(dev, noise_px):
     """Against oracle_pnp_ransac_cv, the restatement that follows OpenCV's epnp.cpp numerics instead
-    of the kernel's (cyclic 12 x 12 Jacobi, SVD beta solves, QR Gauss-Newton, U V^T with OpenCV's det
-    fix, sequential sums) on the same subsets: the inlier count within 8 (with noise: not below the
-    oracle's by more than 8) and R / t within 1e-4 noiseless, 1e-2 with 0.4 px noise (the tolerances of the round-2 test against an SVD-based
-    oracle; the bit-order comparison is test_full_ransac_matches_oracle)."""
-    B, N, S = 16, 1000, 100
+    of the kernel's (cyclic 12 x 12 Jacobi, SVD beta solves, QR Gauss-Newton, R = U V^T of the SVD
+    with the third row negated when det < 0, sequential sums, xc / zc in the inlier test), on the
+    same subsets, both ways.
+
+    Why the counts can differ at all (tests/pnp_divergence.py): a 5-point M is
+    10 x 12, so M^T M has a 2-D exact null space (its two smallest eigenvalues are rounding, ~1e-17
+    of the largest) and the basis an eigen-solver returns for it is decided by its rounding. EPnP's
+    beta approximations 1 and 3 depend on that basis, so Gauss-Newton lands in different minima for
+    ~40 % of noisy hypotheses. Swapping single ingredients of the OpenCV-semantics path for the
+    kernel's shows it is the only cause: with the kernel's null-space basis every hypothesis count
+    agrees (2 of 160 000 differ by rounding at the threshold); the solves (SVD vs Cholesky, QR vs
+    Cholesky) change nothing. cv2's own basis comes from its JacobiSVD's rounding (unpinned here).
+
+    1. Exact, two-sided: with the kernel's null-space basis in the OpenCV-semantics oracle, the GPU's
+       per-hypothesis counts equal it (<= 0.2 % of hypotheses off by <= 2 at the threshold), the
+       selected count is equal in every crop and R / t agree to 1e-4.
+    2. Statistical, two-sided, pure OpenCV numerics: noiseless, every count within 8 and R / t within
+       1e-4; with 0.4 px noise the selected count differs in <= 25 % of crops (CPU study: 10 %), by at
+       most 24 either way (CPU study over 3200 crops: +-22), with |mean gap| <= 2 (no bias: -0.01);
+       R / t within 1e-2 where the selected counts agree."""
+    import ctypes
+
+    B, N, S, H = 64, 1000, 100, 100
     xyz, data, _, _ = _scene(B, N, S, 9, outlier_frac=0.3, noise_px=noise_px)
     # the 256-point selection and the hypothesis subsets from a local generator: the test does not
     # depend on how far earlier tests moved the global CPU / device RNG streams
     g = torch.Generator().manual_seed(2024)
     sel0 = torch.stack([torch.randperm(N, generator=g)[:256] for _ in range(B)]).to(torch.int32)
-    subs0 = torch.stack([torch.stack([torch.randperm(256, generator=g)[:5] for _ in range(100)])
+    subs0 = torch.stack([torch.stack([torch.randperm(256, generator=g)[:5] for _ in range(H)])
                          for _ in range(B)]).to(torch.int32)
     R, t, info = pose.get_pose({"xyz": xyz.to(dev)}, data, sel=sel0, subsets=subs0, return_info=True)
     torch.cuda.synchronize()
     sel = info["sel"].cpu().long()
     subs = info["subsets"].cpu()
-    worst = 0.0
+    hcnt = info["workspace"].cpu()[B * H * 12:].view(torch.int32)[:B * H].view(B, H).numpy()
+    lib = opnp._load()
+    hyp_off = worst_basis = worst = 0.0
+    gaps = []
     for b in range(B):
         s = sel[b]
         pix = data["choose"][b, 0, s]
         obj = (xyz[b].reshape(3, -1)[:, pix].double().t() * data["extent"][b] + data["lfborder"][b]).float().numpy()
         img = np.stack([data["x_map_choosed"][b, s, 0].numpy(), data["y_map_choosed"][b, s, 0].numpy()], 1)
+        gcnt = int(info["inliers"][b])
+        Rg, tg = R[b].cpu().numpy(), t[b].cpu().numpy()
+        lib.oracle_set_cv_variant(ctypes.c_int(1))  # the kernel's null-space basis, OpenCV's numerics otherwise
+        try:
+            cc = _cv_hypothesis_counts(obj, img, subs[b].numpy())
+            Rb, tb, cb, _ = opnp.pnp_ransac_cv(obj, img, K4, subs[b].numpy(), 1.0)
+        finally:
+            lib.oracle_set_cv_variant(ctypes.c_int(0))
+        d = np.abs(cc.astype(int) - hcnt[b])
+        assert d.max() <= 2, (b, d.max())
+        hyp_off += int((d > 0).sum())
+        assert gcnt == cb, (b, gcnt, cb)
+        worst_basis = max(worst_basis, float(np.abs(Rg - Rb).max()), float(np.abs(tg - tb).max()))
         Ro, to, cnt, _ = opnp.pnp_ransac_cv(obj, img, K4, subs[b].numpy(), 1.0)
-        # noiseless: the same count within 8; with noise the two numerics can pick different
-        # hypotheses of the same 100, so the GPU's RANSAC must be at least as good (count >= oracle - 8)
+        gaps.append(gcnt - cnt)
         if noise_px == 0:
-            assert abs(int(info["inliers"][b]) - cnt) <= 8, (b, int(info["inliers"][b]), cnt)
-        else:
-            assert int(info["inliers"][b]) >= cnt - 8, (b, int(info["inliers"][b]), cnt)
-        worst = max(worst, float(np.abs(R[b].cpu().numpy() - Ro).max()), float(np.abs(t[b].cpu().numpy() - to).max()))
-    print(f"noise {noise_px} px: max |dR|, |dt| vs the OpenCV-semantics oracle {worst:.2e}")
-    assert worst < pose_tol, worst
+            assert abs(gcnt - cnt) <= 8, (b, gcnt, cnt)
+        if gcnt == cnt:
+            worst = max(worst, float(np.abs(Rg - Ro).max()), float(np.abs(tg - to).max()))
+    gaps = np.array(gaps)
+    print(f"noise {noise_px} px: kernel-basis oracle: {hyp_off} of {B * H} hypothesis counts off, max |dR|, |dt| "
+          f"{worst_basis:.2e}; OpenCV numerics: selected count differs in {(gaps != 0).sum()} of {B} crops "
+          f"(gaps {gaps[gaps != 0].tolist()}), max |dR|, |dt| where equal {worst:.2e}")
+    assert hyp_off <= 0.002 * B * H, hyp_off
+    assert worst_basis < 1e-4, worst_basis
+    assert (gaps != 0).sum() <= 0.25 * B, gaps
+    assert np.abs(gaps).max() <= 24, gaps
+    assert abs(gaps.mean()) <= 2.0, gaps.mean()
+    assert worst < (1e-4 if noise_px == 0 else 1e-2), worst
+
+
+def _cv_hypothesis_counts(obj, img, subsets, thr=1.0):
+    """Inlier count of every hypothesis under the OpenCV-semantics EPnP (oracle_pnp_hypotheses_diag)."""
+    import ctypes
+    lib = opnp._load()
+    f = lib.oracle_pnp_hypotheses_diag
+    f.restype = None
+    H = len(subsets)
+    R = np.zeros((H, 9), np.float32)
+    t = np.zeros((H, 3), np.float32)
+    cnt = np.zeros(H, np.int32)
+    diag = np.zeros(H, np.int32)
+    sub = np.ascontiguousarray(subsets, np.int32)
+    f(opnp._p(np.ascontiguousarray(obj, np.float32)), opnp._p(np.ascontiguousarray(img, np.float32)),
+      ctypes.c_int(len(obj)), opnp._p(K4), opnp._p(sub), ctypes.c_int(H), ctypes.c_float(thr), ctypes.c_int(1),
+      opnp._p(R), opnp._p(t), opnp._p(cnt), opnp._p(diag))
+    return cnt
