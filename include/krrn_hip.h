@@ -249,19 +249,6 @@ int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, long long v_
                       const float* dn, int S, int C, const float* Y, const float* bn_scale, const float* bn_bias,
                       int relu, float* out, long long o_bs, int o_st, int B, void* stream);
 
-/* Diagnostics: from now on every surface conv (krrn_gcn_conv_f32 with Y == NULL, 3-D, C = 128)
- * writes, per (crop, point, neighbour j), 8 words: the neighbour index, the point's and the
- * neighbour's coordinates as read (f32 bits), the crop; then per block (linear index after the
- * XCD remap) 20 words: digests of the staged directions and of the point directions as the block's
- * LDS holds them before the support loop (4), the XCC id and HW_ID register it ran on (2), the
- * arguments out (2 words), o_bs, o_st, S, relu, dn, v (low words) as the block read them (8), two
- * unused, the same digests after the support loop (4); then per (block, thread, support s < 8)
- * 8 floats: the support's max and the first direction-weight quad as held in registers. Launch i
- * goes into slot i % nslots of `buf` (slot_words u32 each, >= B * n * k * 8 + 20 * nb + 16384 * nb
- * with nb = B * ceil(n / 8) blocks). buf = NULL turns it off; every call resets the launch
- * count. Not for production runs (one host mutex per surface-conv launch). */
-int krrn_gcn_debug(void* buf, int nslots, long long slot_words);
-
 /* Pool_layer max (gcn3d.py:233-236) at the sampled rows only: out[b,t,:] = max_j F[b, nbr[b,t,j], :].
  * C, strides multiple of 4 (float4). */
 int krrn_pool_max_f32(const int* nbr, int nq, int kk, const float* F, long long f_bs, int f_st, int C, float* out,

@@ -17,8 +17,6 @@
 
 #include "krrn_common.h"
 
-#include <mutex>
-
 namespace {
 
 constexpr int kKnnThreads = 256;
@@ -357,7 +355,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
 //     carries no 64-bit address arithmetic (the old form kept ten 64-bit pointers and stepped
 //     them every support: 228 VGPRs, 2 waves per SIMD);
 //   * __launch_bounds__(256, 4): >= 4 waves per SIMD, each with its k gather loads in flight.
-// DBG (diagnostics, krrn_gcn_debug; surface convs only): per-point / per-block records of what the
+// DBG (diagnostics build only, -DKRRN_DIAG=1: krrn_gcn_debug, csrc/krrn_diag.h; surface convs only): per-point / per-block records of what the
 // block read and held in LDS, at the start and at the end of the support loop.
 template <bool HAS_Y, int KC, bool BUF = true, bool DBG = false>
 __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
@@ -543,6 +541,9 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
 
 }  // namespace
 
+#if KRRN_DIAG
+#include "krrn_diag.h"
+#include <mutex>
 namespace {
 // krrn_gcn_debug: where the surface convs (Y == NULL) of the 3-D form dump, per (crop, point,
 // neighbour), the neighbour index and both points' coordinates as the kernel read them (8 words).
@@ -565,6 +566,8 @@ KRRN_API int krrn_gcn_debug(void* buf, int nslots, long long slot_words) {
   g_gcn_dbg.count = 0;
   return KRRN_OK;
 }
+
+#endif  // KRRN_DIAG
 
 KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, long long v_bs, int v_st, int d,
                                const float* dn, int S, int C, const float* Y, const float* bn_scale,
@@ -594,13 +597,16 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   if (use3 && d == 3 && C == 128 && S <= kGcnSmax && (k == 10 || k == 8) &&
       (long long)n * (S + 1) * C * 4 < (1LL << 31)) {
     unsigned* dbg = nullptr;
+#if KRRN_DIAG
     if (!Y && g_gcn_dbg.buf) {
       const std::lock_guard<std::mutex> lk(g_gcn_dbg.mu);
       dbg = g_gcn_dbg.buf + (g_gcn_dbg.count++ % g_gcn_dbg.nslots) * g_gcn_dbg.slot_words;
     }
+#endif
 #define KRRN_GCN3(HY, KC, BF) \
   hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC, BF>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
                      bn_scale, bn_bias, relu, out, o_bs, o_st, dbg)
+#if KRRN_DIAG
     if (dbg) {
       if (k == 10)
         hipLaunchKernelGGL((gcn_conv3_kernel<false, 10, true, true>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs,
@@ -610,6 +616,7 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
                            v_st, dn, S, Y, bn_scale, bn_bias, relu, out, o_bs, o_st, dbg);
       return krrn_launch_status();
     }
+#endif
     if (Y) {
       if (bufload) {
         if (k == 10) KRRN_GCN3(true, 10, true); else KRRN_GCN3(true, 8, true);

@@ -16,7 +16,8 @@
 //     [l] pair per lane, 24 KB at K = 128) are copied into a 2-slot LDS ring one tile ahead by LDS DMA;
 //     every wave reads them with one ds_read_b128 + one ds_read_b64 per group, and the three MFMAs
 //     per 8 k take register slices, W[h l] x A[h h] = hh + lh, W[m h] x A[h m] = mh + hm,
-//     W[m h] x A[m l] = mm + hl; one barrier per tile, two blocks per CU (56 KB LDS, 2 waves per SIMD);
+//     W[m h] x A[m l] = mm + hl; one barrier per tile, two blocks per CU (74 KB LDS per block at K = 128:
+//     48 KB weight ring + 8 KB bias + 18 KB store-transpose slots; 2 waves per SIMD);
 //   * the previous tile's accumulator is stored in the current tile's MFMA gaps as 4 float4 per lane
 //     (operands swapped so a lane holds 4 consecutive columns; transposed through LDS first so each
 //     store instruction writes whole 128-B row segments), bias (from LDS) / residual / ReLU fused.
@@ -68,15 +69,12 @@ __device__ __forceinline__ gp_bf16x8 gp_sub4(const gp_u32x8& c, int o) {
 // that the DMA into one does not alias the reads of the other.
 typedef __attribute__((address_space(3))) void gp_lds_void;
 
-// Transposed stores (KRRN_PANEL_TSTORE, default on; the float4 epilogue only): a lane's accumulator is
+// Transposed stores: a lane's accumulator is
 // 4 float4 of ONE row, so a direct store instruction writes 32 rows x 32 B; the tile instead goes
 // through a per-wave LDS slot and comes back as 8 lanes per row, and each store instruction writes 8
 // whole 128-B row segments. The stores are buffer stores through a per-wave resource bounded by the
 // wave's valid rows: rows past M are dropped by the hardware, so a live wave always issues its 4
 // stores per tile (the vmcnt(4) accounting below depends on it).
-#ifndef KRRN_PANEL_TSTORE
-#define KRRN_PANEL_TSTORE 1
-#endif
 constexpr int kTP = 36;  // LDS pitch of a transposed tile row (floats; conflict-free b128 writes)
 
 template <int KT, bool RES>
@@ -87,10 +85,8 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
   static_assert(NI * 4 * 256 == TILE_U32, "tile DMA split");
   __shared__ __attribute__((aligned(16))) unsigned sbA[TILE_U32];
   __shared__ __attribute__((aligned(16))) unsigned sbB[TILE_U32];
-  __shared__ float sbias[kPanelMaxN];
-#if KRRN_PANEL_TSTORE
+  __shared__ __attribute__((aligned(16))) float sbias[kPanelMaxN];  // read as f32x4 (ds_read_b128)
   __shared__ __attribute__((aligned(16))) float stile[4][32 * kTP];
-#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nl = lane & 31, fh = lane >> 5;
@@ -138,12 +134,7 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
 
   const bool live = m0 < g.M;
   const int rows_left = g.M - m0;
-  const int mrow = nl;
-  float* orow = g.out + (size_t)(m0 + mrow) * g.ldo;
-  const float* rrow = RES ? g.res + (size_t)(m0 + mrow) * g.ldr : nullptr;
-  const bool row_ok = mrow < rows_left;
   f32x4 rv[RES ? 4 : 1];
-#if KRRN_PANEL_TSTORE
   float* const tw = stile[wave];
   const int trow = lane >> 3, tcol = 4 * (lane & 7);  // store j: row 8 j + trow, columns tcol .. + 3
   const int vrows = live ? min(32, rows_left) : 0;
@@ -170,29 +161,6 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[e]), rsO, vo + 4 * e, ctp * 128, 0);
     }
   };
-#endif
-  auto epilogue = [&](const f32x16& acc, int ctp, int q) {
-    if (!row_ok) return;
-    const int n = ctp * 32 + 8 * q + 4 * fh;
-    f32x4 v = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
-    if (g.vec) {
-      v += *reinterpret_cast<const f32x4*>(sbias + n);
-      if constexpr (RES) v += rv[q];
-      if (g.relu) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      *reinterpret_cast<f32x4*>(orow + n) = v;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = v[e] + sbias[n + e];
-        if constexpr (RES) x += rrow[n + e];
-        if (g.relu) x = fmaxf(x, 0.f);
-        orow[n + e] = x;
-      }
-    }
-  };
   f32x16 accp;
 #pragma unroll
   for (int r = 0; r < 16; ++r) accp[r] = 0.f;
@@ -200,7 +168,6 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
   auto step = [&](int ct, const unsigned* cur, unsigned* nxt) {
     const bool has = ct < ct1;
     const bool st = live && ct > ct0;
-#if KRRN_PANEL_TSTORE
     if (st) {
       // tile ct - 1 through the wave's LDS slot: written as (row nl, columns 8 q + 4 fh), read back as
       // (row 8 j + trow, columns tcol); the slot is this wave's alone and a wave's LDS accesses stay in order
@@ -226,14 +193,6 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
         }
       }
     }
-#else
-    if constexpr (RES) {
-      if (g.vec && st && row_ok) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rv[q] = *reinterpret_cast<const f32x4*>(rrow + (ct - 1) * 32 + 8 * q + 4 * fh);
-      }
-    }
-#endif
     if (ct + 1 < ct1) dma_tile(ct + 1, nxt);  // its last readers (tile ct - 1) passed the previous barrier
     f32x16 acc;
 #pragma unroll
@@ -249,11 +208,7 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(mh), gp_sub4(ca[gi], 2), acc, 0, 0, 0);  // mh + hm
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gp_op(mh), gp_sub4(ca[gi], 4), acc, 0, 0, 0);  // mm + hl
       }
-#if KRRN_PANEL_TSTORE
       if (st && gi % (G / 4) == 0) epilogue_t(ct - 1, gi / (G / 4));
-#else
-      if (st && gi % (G / 4) == 0) epilogue(accp, ct - 1, gi / (G / 4));
-#endif
     }
     accp = acc;
     // this wave's DMA into nxt must have landed before any wave reads it: vmcnt retires in order and

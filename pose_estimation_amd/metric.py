@@ -31,11 +31,14 @@ def add_metric(pred_r: torch.Tensor, pred_t: torch.Tensor, model_points: torch.T
         raise RuntimeError("add_metric runs on the HIP path only (GPU tensors)")
     B, Pn = model_points.shape[0], model_points.shape[1]
     f = lambda x: h2d(x, dev, torch.float32)  # noqa: E731
+    # every converted operand stays bound until the launch is enqueued: a temporary freed after
+    # ptr() could hand its caching-allocator block to the next conversion before the kernel reads it
+    r, t, mp, tg = f(pred_r).reshape(B, 9), f(pred_t).reshape(B, 3), f(model_points), f(target)
+    cls = h2d(cls_id.reshape(B), dev, torch.int64)
     symt = h2d(torch.tensor(list(sym) or [0], dtype=torch.int32), dev)
     ws = torch.empty((B * ((Pn + 255) // 256),), dtype=torch.float64, device=dev)
     out = torch.empty((B,), dtype=torch.float64, device=dev)
-    _lib.call("krrn_add_metric_f32", ptr(f(pred_r).reshape(B, 9)), ptr(f(pred_t).reshape(B, 3)), ptr(f(model_points)),
-              ptr(f(target)), ptr(h2d(cls_id.reshape(B), dev, torch.int64)), ptr(symt),
+    _lib.call("krrn_add_metric_f32", ptr(r), ptr(t), ptr(mp), ptr(tg), ptr(cls), ptr(symt),
               len(sym), B, Pn, ptr(ws), ptr(out), P(torch.cuda.current_stream(dev).cuda_stream))
     return out
 

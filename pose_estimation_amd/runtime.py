@@ -29,7 +29,6 @@ U = ctypes.c_uint
 # C-ABI signatures (include/krrn_hip.h); every function returns int status.
 _lib.register("krrn_knn_f32", [P, L, I, I, P, P, L, I, I, I, I, I, I, I, P, P])
 _lib.register("krrn_gcn_conv_f32", [P, I, I, P, L, I, I, P, I, I, P, P, P, I, P, L, I, I, P])
-_lib.register("krrn_gcn_debug", [P, I, L])
 _lib.register("krrn_pool_max_f32", [P, I, I, P, L, I, I, P, L, I, I, P])
 _lib.register("krrn_resize_bilinear_f32", [P, I, I, I, I, I, I, P, I, I, I, I, P, I, I, I, I, P])
 _lib.register("krrn_add_relu_f32", [P, I, I, P, I, I, P, I, I, L, I, I, P])
@@ -476,16 +475,17 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
     the A-stationary split-bf16 kernel and K >= 256 ones to gemm_x3 first (own kernels).
     require_x3: only gemm_x3 will do (its ldr = 0 per-group row broadcast); False if ineligible.
     blas_ok=False: own kernels only (False instead of a hipBLASLt plan).
-    A K = 128 GEMM with a residual is not taken by the panel kernel: its register-only form (the only
-    one with room for the residual at K = 128) is kept for diagnostics."""
+    A K = 128 GEMM with a residual is not taken by the panel kernel (its 128-VGPR activation chain
+    leaves no room for the residual tile; krrn_gemm_panel_x3_f32 returns KRRN_EUNSUPPORTED), nor is
+    one wider than the kernel's 2048-column bias stage (KRRN_ESHAPE)."""
     dev = plan.device
     w = wt.reshape(N, -1)[:, :K].float()
     if scale is not None:
         w = w * scale.reshape(N, 1).to(w.device)
     w = w.contiguous()
     flops = 2.0 * (cin or K) * (cout or N) * M * batch
-    if GEMM_PANEL and not require_x3 and K in (64, 128) and N % 32 == 0 and batch == 1 and lda % 4 == 0 \
-            and a_off % 4 == 0 and not (K == 128 and res is not None):
+    if GEMM_PANEL and not require_x3 and K in (64, 128) and N % 32 == 0 and N <= 2048 and batch == 1 \
+            and lda % 4 == 0 and a_off % 4 == 0 and not (K == 128 and res is not None):
         wp = ops.gemm_weights_panel(w)
         plan.buffers.append([wp, bias])
         csplit = 1

@@ -16,11 +16,17 @@ graph half-step both slots' F0 and shadows are filled with sentinels (-7 / -9): 
 from the same inputs each rep, so a lost store or a read of a stale copy would otherwise show the
 previous rep's identical value; with the sentinel, a store that never reached memory reads -7.
 
-usage (GPU box): KRRN_STREAMS=1 python3 profiles/f0_shadow.py [REPS] [--history]"""
+usage (GPU box, the diagnostics build of the library):
+  make -C pose_estimation_amd/csrc diag
+  KRRN_STREAMS=1 python3 profiles/f0_shadow.py [REPS] [--history]"""
+import ctypes
 import os
 import sys
 
 os.environ.setdefault("KRRN_STREAMS", "1")
+# krrn_gcn_debug exists only in the diagnostics build (csrc/krrn_diag.h)
+os.environ.setdefault("KRRN_HIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "build", "diag", "libkrrn_hip_diag.so"))
 import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -30,6 +36,8 @@ from pose_estimation_amd import KRRN, _lib, make_config  # noqa: E402
 from pose_estimation_amd.pipeline import PipelinedPipeline, _sub_plan  # noqa: E402
 from pose_estimation_amd.runtime import Late, Op, P, ptr, _skey  # noqa: E402
 from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
+
+_lib.register("krrn_gcn_debug", [P, ctypes.c_int, ctypes.c_longlong])
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 REPS = int(args[0]) if args else 5

@@ -119,6 +119,36 @@ def test_gemm_panel_vs_torch(dev, M, K, N, lda, a_off, relu, with_res, csplit):
     assert torch.all(out[:, N:] == 7.0), "wrote past N"
 
 
+@pytest.mark.parametrize("M,K,N,ldo,ldr,out_off,with_res", [
+    (77, 128, 96, 101, 0, 0, False),   # ldo % 4 != 0, row tail
+    (77, 64, 96, 100, 99, 0, True),    # ldr % 4 != 0 with the residual, row tail
+    (130, 64, 64, 68, 68, 1, True),    # out one float off 16-B alignment, residual, row tail
+    (130, 128, 128, 132, 0, 3, False)])  # out three floats off, K = 128
+def test_gemm_panel_scalar_epilogue(dev, M, K, N, ldo, ldr, out_off, with_res):
+    """The g.vec == 0 epilogue of krrn_gemm_panel_x3_f32 (output / residual not float4-addressable:
+    dword stores, scalar residual reads) vs torch f64, and nothing written outside the out view."""
+    g = torch.Generator().manual_seed(M + K + N + ldo)
+    A = torch.randn(M, K + 4, generator=g).to(dev)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(dev)
+    bias = (0.1 * torch.randn(N, generator=g)).to(dev)
+    res = torch.randn(M * ldr + 8, generator=g).to(dev) if with_res else None
+    buf = torch.full((out_off + M * ldo + 8,), 7.0, device=dev)
+    wp = ops.gemm_weights_panel(W)
+    st = _lib.lib().krrn_gemm_panel_x3_f32(ptr(A), K + 4, M, K, N, ptr(wp), ptr(bias), ptr(res), ldr,
+                                          P(buf.data_ptr() + 4 * out_off), ldo, 1, 1,
+                                          P(torch.cuda.current_stream().cuda_stream))
+    _lib.check(st, "gemm_panel_x3 (scalar epilogue)")
+    torch.cuda.synchronize()
+    ref = A[:, :K].double() @ W.double().t() + bias.double()
+    if with_res:
+        ref = ref + res[:M * ldr].view(M, ldr)[:, :N].double()
+    ref = ref.clamp_min(0)
+    got = buf[out_off:out_off + M * ldo].view(M, ldo)
+    err = float((got[:, :N].double() - ref).abs().max())
+    assert err <= 2e-6 * float(ref.abs().max()), err
+    assert torch.all(got[:, N:] == 7.0) and torch.all(buf[:out_off] == 7.0) and torch.all(buf[out_off + M * ldo:] == 7.0)
+
+
 def test_gemm_panel_rejects(dev):
     A = torch.zeros(64, 128, device=dev)
     W = torch.zeros(128, 128, device=dev)
@@ -131,8 +161,7 @@ def test_gemm_panel_rejects(dev):
     assert L.krrn_gemm_panel_x3_f32(P(A.data_ptr() + 4), 128, 64, 128, 128, ptr(wp), P(0), P(0), 0, ptr(out), 128, 0,
                                     1, s) < 0
     assert L.krrn_gemm_panel_x3_f32(P(0), 128, 64, 128, 128, ptr(wp), P(0), P(0), 0, ptr(out), 128, 0, 1, s) < 0
-    # K = 128 with a residual: only the register-only form has room for it, and that form is
-    # diagnostics-only: refused
+    # K = 128 with a residual: the 128-VGPR activation chain leaves no room for the residual tile: refused
     assert L.krrn_gemm_panel_x3_f32(ptr(A), 128, 64, 128, 128, ptr(wp), P(0), ptr(out), 128, ptr(out), 128, 0, 1,
                                     s) == -4
 
