@@ -155,10 +155,14 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
     const unsigned vo = (unsigned)(((8 * j + trow) * g.ldo + tcol) * 4);
     if (g.vec) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gp_u32x4, v), rsO, vo, ctp * 128, 0);
-    } else {  // out / ldo not 16-B aligned: four dword stores
+    } else {
+      // out / ldo not 16-B aligned: four dword stores. (Not __builtin_bit_cast(unsigned, v[e]): on an
+      // ext_vector element clang (ROCm 7.2) reads element 0 whatever e is -- the IR extracts lane 0 for
+      // all four -- so this path stored v[0] four times; found by
+      // tests/test_gpu_gemm.py::test_gemm_panel_scalar_epilogue.)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[e]), rsO, vo + 4 * e, ctp * 128, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[e]), rsO, vo + 4 * e, ctp * 128, 0);
     }
   };
   f32x16 accp;

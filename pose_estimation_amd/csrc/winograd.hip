@@ -113,8 +113,20 @@ __device__ __forceinline__ void wino_epi_put(float* smem, f32x16 (&acc)[4][kNJ])
 constexpr int kGX = 16, kGY = 2;                 // tiles per block (x, y): kGX * kGY == kWT
 constexpr int kRR = 2 * kGY + 2, kRC = 2 * kGX + 2;  // raw rows / cols of a block
 constexpr int kRPieces = kRR * kRC * 2;          // 16-B pieces per chunk
-constexpr int kRSlot = 512 * 4;                  // floats per ring slot (2 pieces per thread)
 static_assert(kGX * kGY == kWT && kRPieces <= 512, "ring geometry");
+// Ring slot layout: piece (raw row r, column c, channel half h) at 16-B slot r * kRowSlots + 2c + h +
+// c / 2 (one slot of padding per column pair). A wave's ds_read_b128 of patch column j reads, per
+// lane (tile tx, ty; half h), slot (2 ty + row) * kRowSlots + 5 tx + h + {0, 2, 5, 7}[j]: the 16 lanes
+// of each b128 lane group land on 16 distinct 16-B bank slots (kRowSlots = 88 >= the 85 slots of a padded
+// row, and = 0 mod 8, which keeps the two tile rows apart). Unpadded (2c + h) they shared 4 bank slots: 4-way conflicts, 62 % of the kernel's
+// LDS-array cycles (profiles/r4_wino_pmc.sh, SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE).
+constexpr int kRowSlots = 88;
+constexpr int kColOff[4] = {0, 2, 5, 7};
+constexpr int kRSlot = kRR * kRowSlots * 4;      // floats per ring slot
+constexpr int kRDummy = kRR * kRowSlots - 1;     // the slot threads without a piece write to
+__device__ __forceinline__ int ring_slot(int r, int c, int h) { return r * kRowSlots + 2 * c + h + (c >> 1); }
+static_assert(2 * (kRC - 1) + 1 + (kRC - 1) / 2 < kRowSlots && (kRowSlots % 8) == 0, "padded ring row");
+static_assert((kRR - 1) * kRowSlots + 2 * (kRC - 1) + 1 + (kRC - 1) / 2 < kRDummy, "padded ring slot fits");
 static_assert(4 * 2 * kWT * kSP >= 3 * kRSlot, "ring fits in the epilogue's LDS");
 
 // epilogue finish for a 2-D tile block: tile tl -> (ty, tx) = (tl / kGX, tl % kGX)
@@ -206,10 +218,17 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
     for (int i = 0; i < 2; ++i)
       r[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, (roff[i] + cb) | cm, 0, 0));
   };
+  int wslot[2];  // this thread's 2 pieces in the padded slot layout (pieces past the region: a dummy slot)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + 256 * i;
+    const int pix = q >> 1, rr = pix / kRC;
+    wslot[i] = q < kRPieces ? ring_slot(rr, pix - rr * kRC, q & 1) : kRDummy;
+  }
   auto store_raw = [&](int slot, const f32x4 (&r)[2]) {
     float* dst = smem + slot * kRSlot;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dst + 4 * (tid + 256 * i)) = r[i];
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dst + 4 * wslot[i]) = r[i];
   };
 
   // weights of this wave's components: lane (n = j*32 + fr, channels 4h..4h+3) of U[ck][xi][n]
@@ -240,8 +259,8 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
   const int rb = wave == 0 ? 2 : (wave == 3 ? 3 : (wave == 1 ? 2 : 1));
   const float sgn = wave == 1 ? 1.f : -1.f;
   const int tx = fr % kGX, ty = fr / kGX;
-  const int pa = ((2 * ty + ra) * kRC + 2 * tx) * 2 + h;  // piece index of (row ra, col 0)
-  const int pb = ((2 * ty + rb) * kRC + 2 * tx) * 2 + h;
+  const int pa = ring_slot(2 * ty + ra, 2 * tx, h);  // slot of (row ra, patch column 0)
+  const int pb = ring_slot(2 * ty + rb, 2 * tx, h);
 
   f32x16 acc[4][kNJ];
 #pragma unroll
@@ -255,8 +274,8 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
     f32x4 t[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const f32x4 da = *reinterpret_cast<const f32x4*>(sl + 4 * (pa + 2 * c));
-      const f32x4 db = *reinterpret_cast<const f32x4*>(sl + 4 * (pb + 2 * c));
+      const f32x4 da = *reinterpret_cast<const f32x4*>(sl + 4 * (pa + kColOff[c]));
+      const f32x4 db = *reinterpret_cast<const f32x4*>(sl + 4 * (pb + kColOff[c]));
       t[c] = da + sgn * db;
     }
     V[0] = t[0] - t[2];
@@ -411,10 +430,17 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
       r[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, half ? roffm[i] : roff[i],
                                                                             ck * kWC * 4, 0));
   };
+  int wslot[2];  // this thread's 2 pieces in the padded slot layout (pieces past the region: a dummy slot)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + 256 * i;
+    const int pix = q >> 1, rr = pix / kRC;
+    wslot[i] = q < kRPieces ? ring_slot(rr, pix - rr * kRC, q & 1) : kRDummy;
+  }
   auto store_raw = [&](int slot, const f32x4 (&r)[2]) {
     float* dst = smem + slot * kRSlot;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dst + 4 * (tid + 256 * i)) = r[i];
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<f32x4*>(dst + 4 * wslot[i]) = r[i];
   };
 
   // split weights, record (chunk, xi, n, half): 16 B of plane U_mh, 8 B of plane U_l. Lanes of n
@@ -448,8 +474,8 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
   const int ra = wave == 0 ? 0 : (wave == 2 ? 2 : 1);
   const int rb = wave == 0 ? 2 : (wave == 3 ? 3 : (wave == 1 ? 2 : 1));
   const int tx = fr % kGX, ty = fr / kGX;
-  const int pa = ((2 * ty + ra) * kRC + 2 * tx) * 2 + h;
-  const int pb = ((2 * ty + rb) * kRC + 2 * tx) * 2 + h;
+  const int pa = ring_slot(2 * ty + ra, 2 * tx, h);  // slot of (row ra, patch column 0)
+  const int pb = ring_slot(2 * ty + rb, 2 * tx, h);
 
   f32x16 acc[4][kNJ];
 #pragma unroll
@@ -465,8 +491,8 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
     f32x4 t[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const f32x4 da = *reinterpret_cast<const f32x4*>(sl + 4 * (pa + 2 * c));
-      const f32x4 db = *reinterpret_cast<const f32x4*>(sl + 4 * (pb + 2 * c));
+      const f32x4 da = *reinterpret_cast<const f32x4*>(sl + 4 * (pa + kColOff[c]));
+      const f32x4 db = *reinterpret_cast<const f32x4*>(sl + 4 * (pb + kColOff[c]));
 #pragma unroll
       for (int e = 0; e < 4; ++e) t[c][e] = __builtin_fmaf(sgn, db[e], da[e]);
     }
