@@ -21,6 +21,8 @@ activation.
 """
 from __future__ import annotations
 
+import os
+
 import math
 from typing import Callable, Dict, List, Optional
 
@@ -89,6 +91,8 @@ class FusionNetLite(nn.Module):
 
 
 FEAT_SID = 4  # plan stream of the materialised output concat (joined by the caller)
+# crops per chunk of the level-0 GEMM + gather-conv (0: the whole batch in one launch each)
+FUSION_CHUNK = int(os.environ.get("KRRN_FUSION_CHUNK", "0"))
 
 def level_sizes(N: int, k0: int):
     N1 = int(N / 4)
@@ -132,8 +136,13 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     i32 = torch.int32
     idx0 = plan.buf((B, N, k0), i32)
     F0 = plan.buf((B, N, 384))
-    # one GEMM-output buffer per branch: the three branches run on their own plan streams
-    Y1 = [plan.buf((B * N, (S + 1) * 128)) for _ in range(3)]
+    # one GEMM-output buffer per branch: the three branches run on their own plan streams. With
+    # FUSION_CHUNK = c the level-0 GEMM and its gather-conv run in crop chunks of c through a
+    # c-crop buffer per branch (crops are independent: a point's neighbours are in its own crop),
+    # so Y is written and re-read while it sits in the Infinity Cache instead of one 262 MB HBM
+    # round trip per branch; the buffer is reused by every chunk
+    cy = B if not FUSION_CHUNK or FUSION_CHUNK >= B else FUSION_CHUNK
+    Y1 = [plan.buf((cy * N, (S + 1) * 128)) for _ in range(3)]
     feat1 = plan.buf((B, N, 384))
     nb4 = {br: plan.buf((B, N1, 4), i32) for br in ("v", "x", "n")}
     V1 = plan.buf((B, N1, 9))
@@ -157,12 +166,12 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     def knn(q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, out):
         plan.add("krrn_knn_f32", q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, B, ptr(out))
 
-    def gcn(idx, n, k, v, v_bs, d, dn, C, Y, bn, relu, out, o_bs, o_st):
+    def gcn(idx, n, k, v, v_bs, d, dn, C, Y, bn, relu, out, o_bs, o_st, Bc=None):
         keep.append(dn)
         s, b = (None, None) if bn is None else bn
         keep.extend([s, b])
         plan.add("krrn_gcn_conv_f32", ptr(idx), n, k, v, v_bs, 9, d, ptr(dn), S, C, ptr(Y), ptr(s), ptr(b), int(relu),
-                 out, o_bs, o_st, B)
+                 out, o_bs, o_st, B if Bc is None else Bc)
 
     def gemm(a, a_cs, a_co, M, layer: Conv_layer, out):
         spec = ops.make_linear(layer.weights.detach().t(), layer.bias, None, dev,
@@ -192,9 +201,12 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
             gcn(idx0, N, k0, off(p9, 3 * bi), N * 9, 3, _dn(c0.directions, dev), 128, None, None, True,
                 off(F0, 128 * bi), N * 384, 384)
             c1 = getattr(fu, f"conv_1_{br}")
-            gemm(F0, 384, 128 * bi, B * N, c1, Y1[bi])
-            gcn(idx0, N, k0, off(p9, 3 * bi), N * 9, 3, _dn(c1.directions, dev), 128, Y1[bi],
-                _bn1d(getattr(fu, f"bn1_{br}"), dev), True, off(feat1, 128 * bi), N * 384, 384)
+            dn1, bn1 = _dn(c1.directions, dev), _bn1d(getattr(fu, f"bn1_{br}"), dev)
+            for b0 in range(0, B, cy):
+                nb = min(cy, B - b0)
+                gemm(F0[b0:b0 + nb], 384, 128 * bi, nb * N, c1, Y1[bi])
+                gcn(idx0[b0:b0 + nb], N, k0, off(p9[b0:], 3 * bi), N * 9, 3, dn1, 128, Y1[bi], bn1, True,
+                    off(feat1[b0:], 128 * bi), N * 384, 384, Bc=nb)
             # pools (fusion.py:197-202): kNN(4) at the sampled rows, max, vertex gather
             perm = perms[br]
             knn(off(p9, 3 * bi), N * 9, 9, N1, ptr(perm), off(p9, 3 * bi), N * 9, 9, N, 3, 4, 1, 0, nb4[br])

@@ -50,6 +50,10 @@ NCHW_X3 = os.environ.get("KRRN_NCHW_X3", "1") == "1"
 
 
 TBASE_EARLY = os.environ.get("KRRN_TBASE_EARLY", "1") == "1"
+# crops per chunk of the heads' full-resolution tail (x2 upsample + the S-px convs + final 1x1): each
+# chunk's maps (7.4 MB per crop and map at S = 120) are written and re-read through reused chunk
+# buffers while they sit in the Infinity Cache, instead of B-crop round trips through HBM (0: off)
+HEAD_CHUNK = int(os.environ.get("KRRN_HEAD_CHUNK", "0"))
 # KRRN.forward replays a hipGraph of its plan (captured after one serial warm-up run): the only
 # form in which the plan's side streams run concurrently (runtime.Plan); 0 = serial eager runs
 GRAPH = os.environ.get("KRRN_GRAPH", "1") == "1"
@@ -92,25 +96,18 @@ class KRRNPlan:
         X = model.XYZNet
         h = bld.conv(xmap, X[0], X[1], relu=True)
         h = bld.conv(h, X[3], X[4], relu=True)
-        h = bld.conv_up2(h, X[7], X[8], relu=True)
-        h = bld.conv(h, X[10], X[11], relu=True)
         self.xyz_outc = model.xyz_outc
-        self.fx = plan.buf((B, model.xyz_outc, h.H, h.W))
-        spec = ops.make_conv(model.xyz_final, None, device, cin_p=h.cp)
-        bld.specs.append(spec)
-        self._nchw_conv(h, spec, self.fx, model.xyz_outc)
+        Ho, Wo = 2 * h.H, 2 * h.W
+        self.fx = plan.buf((B, model.xyz_outc, Ho, Wo))
+        self._head_tail(bld, h, [(X[7], X[8]), (X[10], X[11])], model.xyz_final, self.fx, model.xyz_outc)
         # NMLNet (krrn.py:68-84)
         Nn = model.NMLNet
         with plan.on_stream(1):
             g = bld.conv(ymap, Nn[0], Nn[1], relu=True)
             g = bld.conv(g, Nn[3], Nn[4], relu=True)
-            g = bld.conv_up2(g, Nn[7], Nn[8], relu=True)
-            self.fn = plan.buf((B, 3 * C, g.H, g.W))
-            spec_n = ops.make_conv(model.nml_final, None, device, cin_p=g.cp)
-            bld.specs.append(spec_n)
-            self._nchw_conv(g, spec_n, self.fn, 3 * C)
+            self.fn = plan.buf((B, 3 * C, Ho, Wo))
+            self._head_tail(bld, g, [(Nn[7], Nn[8])], model.nml_final, self.fn, 3 * C)
         plan.join([1])
-        Ho, Wo = h.H, h.W
         self.Ho, self.Wo = Ho, Wo
         # class gather + F.normalize (krrn.py:100-108)
         self.xyz = plan.buf((B, 3, Ho, Wo))
@@ -201,6 +198,36 @@ class KRRNPlan:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.warm = False
         self.nbytes = plan_bytes(plan) + plan_bytes(getattr(self, "device_perm_plan", None))
+
+    def _head_tail(self, bld: _Builder, x: Act, convs, final: nn.Conv2d, out: torch.Tensor, n_store: int):
+        """A head's full-resolution tail (krrn.py:56-65 / 78-84): UpsamplingBilinear2d(x2) ->
+        [conv3x3 + BN + ReLU] x len(convs) -> the final 1x1 (+ bias) into the NCHW map `out`, the
+        upsample folded as the first conv's input (conv_up2). With HEAD_CHUNK = c the crops run in
+        chunks of c through c-crop buffers that every chunk reuses (the same kernels per crop)."""
+        B = x.B
+        c = B if not HEAD_CHUNK or HEAD_CHUNK >= B else HEAD_CHUNK
+        spec = ops.make_conv(final, None, self.plan.device, cin_p=pad4(convs[-1][0].out_channels))
+        bld.specs.append(spec)
+        if c == B:
+            h = bld.conv_up2(x, convs[0][0], convs[0][1], relu=True)
+            for conv, bn in convs[1:]:
+                h = bld.conv(h, conv, bn, relu=True)
+            self._nchw_conv(h, spec, out, n_store)
+            return
+        H, W = 2 * x.H, 2 * x.W
+        cb = _Builder(self.plan, c)
+        cb.specs = bld.specs
+        up = cb.act(H, W, x.c)
+        mids = [cb.act(H, W, conv.out_channels) for conv, _ in convs]
+        for b0 in range(0, B, c):
+            nb = min(c, B - b0)
+            xv = Act(x.t[b0:b0 + nb], nb, x.H, x.W, x.cs, x.co, x.c)
+            uv = Act(up.t[:nb], nb, H, W, up.cs, up.co, up.c)
+            cb.resize(xv, uv, align=True)
+            h = uv
+            for (conv, bn), m in zip(convs, mids):
+                h = cb.conv(h, conv, bn, out=Act(m.t[:nb], nb, H, W, m.cs, m.co, m.c), relu=True)
+            self._nchw_conv(h, spec, out[b0:b0 + nb], n_store)
 
     def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):
         """The heads' final 1x1 conv + bias written NCHW (krrn.py:97-98, 80-84):
