@@ -224,19 +224,6 @@ typedef struct krrn_small_desc {
 } krrn_small_desc;
 int krrn_conv_small_group_f32(const krrn_small_desc* descs, int n, void* stream);
 
-/* HRNet branch chain (myhrnet.py:34-63 BasicBlock, :226-231 branches[i](x[i])): `nconv` / 2
- * BasicBlocks (conv3x3 + BN + ReLU, conv3x3 + BN + residual + ReLU; stride 1, cp channels in and
- * out) of one branch in ONE launch, replacing nconv krrn_conv_small_f32 launches. One workgroup per
- * image keeps the image's map and the block intermediate in LDS for the whole chain. in / out: NHWC
- * [B][H][W][*_cs], channels [*_co, *_co + cp) (cp = physical channels, pad channels zero); per conv c:
- * wt[c] = ops.chain_weights_x3 planes of the [cp][9 cp] packed weights (k = tap * cp + channel),
- * scale[c] / bias[c] = cp floats of folded eval BN. Split-bf16 products (f32 accurate, f32
- * accumulation). KRRN_ESHAPE / KRRN_EUNSUPPORTED when the two maps do not fit in LDS or no tile
- * configuration covers the map (krrn_hr_chain_query answers that without launching). */
-int krrn_hr_chain_query(int H, int W, int cp);
-int krrn_hr_chain_f32(const float* in, int in_cs, int in_co, float* out, int out_cs, int out_co, int B, int H, int W,
-                      int cp, int nconv, const void* const* wt, const float* const* scale, const float* const* bias,
-                      void* stream);
 
 /* k nearest neighbours without the [n, n] distance matrix.
  * Replaces gcn3d.get_neighbor_index (gcn3d.py:15-26; mode 0, drop_first = 1: topk(k+1)[1:])

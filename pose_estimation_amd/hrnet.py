@@ -20,14 +20,13 @@ pad channels are exactly zero and the packed weights map logical -> physical cha
 """
 from __future__ import annotations
 
-import ctypes
 import os
 from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
 
-from . import _lib, ops
+from . import ops
 from .config import load_hrnet_spec
 from .ops import Act, pad4
 from .runtime import add_conv_group, add_gemm, add_small_group, Plan, add_conv, ptr
@@ -35,9 +34,6 @@ from .runtime import add_conv_group, add_gemm, add_small_group, Plan, add_conv, 
 # HRNet branch convs as per-branch chains on plan streams (KRRN_HR_GROUP=0) or as grouped
 # launches, one per block depth (KRRN_HR_GROUP=1)
 HR_GROUP = os.environ.get("KRRN_HR_GROUP", "0") == "1"
-# a module's BasicBlocks on one branch as ONE krrn_hr_chain_f32 launch (the image's maps LDS-resident
-# through the whole chain) wherever the two maps fit in LDS; KRRN_HR_CHAIN=0: per-conv launches
-HR_CHAIN = os.environ.get("KRRN_HR_CHAIN", "0") == "1"
 # deconv_layer folded through the linear last_layer_2 (build_hrnet_plan)
 DECONV_FOLD = os.environ.get("KRRN_DECONV_FOLD", "1") == "1"
 # transposed convs (4 parity-class convs) as one grouped launch
@@ -410,48 +406,6 @@ class _Builder:
         res = x if blk.downsample is None else self.conv(x, blk.downsample[0], blk.downsample[1])
         return self.conv(h, blk.conv2, blk.bn2, out=out, res=res, relu=True)
 
-    def branch_chain(self, x: Act, blocks) -> Optional[Act]:
-        """All of a branch's BasicBlocks (myhrnet.py:34-63, 226-231) as ONE krrn_hr_chain_f32 launch,
-        or None (nothing emitted) when a block has a downsample / changes width, or the image's two
-        maps do not fit in LDS (krrn_hr_chain_query)."""
-        blocks = list(blocks)
-        cp = x.cp
-        if not blocks or 2 * len(blocks) > 8 or x.co % 4 or x.cs % 4:
-            return None
-        for blk in blocks:
-            if not isinstance(blk, BasicBlock) or blk.downsample is not None:
-                return None
-            for conv in (blk.conv1, blk.conv2):
-                if conv.in_channels != x.c or conv.out_channels != x.c or conv.stride != (1, 1) \
-                        or conv.kernel_size != (3, 3):
-                    return None
-        if _lib.lib().krrn_hr_chain_query(x.H, x.W, cp) != 0:
-            return None
-        out = self.act(x.H, x.W, x.c)
-        wts, scs, bis = [], [], []
-        flops = mfma = 0.0
-        for blk in blocks:
-            for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
-                spec = ops.make_conv(conv, bn, self.dev, cin_p=cp)
-                w3 = ops.chain_weights_x3(spec.wt[0], cp)
-                self.specs.extend([spec, w3])
-                wts.append(w3.data_ptr())
-                scs.append(spec.scale.data_ptr())
-                bis.append(spec.bias.data_ptr())
-                M = x.B * x.H * x.W
-                flops += 2.0 * spec.cin * spec.cout * 9 * M
-                nt, steps = (cp + 15) // 16, (9 * cp // 4 + 3) // 4
-                mfma += 2.0 * 16 * 16 * 16 * nt * steps * ((x.H * x.W + 15) // 16) * x.B * 6 / 16
-        n = len(wts)
-        arrs = ((ctypes.c_void_p * n)(*wts), (ctypes.c_void_p * n)(*scs), (ctypes.c_void_p * n)(*bis))
-        self.plan.buffers.append(arrs)
-        self.plan.add("krrn_hr_chain_f32", ptr(x.t), x.cs, x.co, ptr(out.t), out.cs, out.co, x.B, x.H, x.W, cp, n,
-                      ctypes.cast(arrs[0], ctypes.c_void_p), ctypes.cast(arrs[1], ctypes.c_void_p),
-                      ctypes.cast(arrs[2], ctypes.c_void_p),
-                      meta=dict(kernel="hr_chain", flops=flops, tag="hr_branch_chain", M=x.B * x.H * x.W, N=cp,
-                                K=9 * cp, splits=1, mfma_flops=mfma))
-        return out
-
     def bottleneck(self, x: Act, blk: Bottleneck) -> Act:
         h = self.conv(x, blk.conv1, blk.bn1, relu=True)
         h = self.conv(h, blk.conv2, blk.bn2, relu=True)
@@ -473,11 +427,9 @@ class _Builder:
             plan.fork(side)
             for i, x in enumerate(xs):
                 with plan.on_stream(i):
-                    y = self.branch_chain(x, m.branches[i]) if HR_CHAIN else None
-                    if y is None:
-                        y = x
-                        for blk in m.branches[i]:
-                            y = self.basic(y, blk)
+                    y = x
+                    for blk in m.branches[i]:
+                        y = self.basic(y, blk)
                 ys.append(y)
             plan.join(side)
         if nb == 1:

@@ -312,23 +312,6 @@ def quad_weights_x3(wt: torch.Tensor, N: int, K: int, kq_mult: int = 4) -> torch
     return torch.cat([mh, lp]).contiguous()
 
 
-def chain_weights_x3(wt: torch.Tensor, cp: int) -> torch.Tensor:
-    """3x3 conv weights [>= cp][9 cp] f32 (k = tap * cp + c, ops.make_conv's packing) -> the split
-    planes krrn_hr_chain_f32 reads (the MFMA's first operand, lane-linear): int32 [NT][S][64][4] =
-    per (16-channel output tile t, 16-channel k-step s) 64 lanes x [m0..m3 h0..h3] bf16, then
-    [NT][S][64][2] = [l0..l3]; lane g * 16 + r holds output channel 16 t + r and k-quad 4 s + g
-    (channels 4 (4 s + g) .. + 3 of the flattened k). Zero past cp output channels / 9 cp k."""
-    NT = (cp + 15) // 16
-    S = (9 * cp // 4 + 3) // 4
-    w = torch.zeros(NT * 16, S * 16, dtype=torch.float32, device=wt.device)
-    n = min(wt.shape[0], cp)
-    w[:n, :9 * cp] = wt.reshape(wt.shape[0], -1)[:n, :9 * cp].float()
-    h, m, l = (t.reshape(NT, 16, S, 4, 4) for t in split_bf16x3(w))          # t r s g ch
-    mh = torch.cat([m, h], dim=-1).permute(0, 2, 3, 1, 4).contiguous()        # t s g r 8
-    lp = l.permute(0, 2, 3, 1, 4).contiguous()                               # t s g r 4
-    return torch.cat([mh.view(torch.int32).reshape(-1), lp.view(torch.int32).reshape(-1)]).contiguous()
-
-
 def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:
     """GEMM weights [N][K] f32 (scale folded) -> the layout krrn_gemm_panel_x3_f32 reads: int32
     [N/32][K/8][384]; per (column tile nb, 8-k group g) 64 lanes x [m0..m3

@@ -53,8 +53,6 @@ _lib.register("krrn_conv1x1_nchw_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I
 _lib.register("krrn_conv1x1_nchw_x3_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
 _lib.register("krrn_conv_small_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, I, I, I, I, P])
 _lib.register("krrn_conv_small_group_f32", [P, I, P])
-_lib.register("krrn_hr_chain_query", [I, I, I])
-_lib.register("krrn_hr_chain_f32", [P, I, I, P, I, I, I, I, I, I, I, P, P, P, P])
 _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L, P, P])
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])

@@ -461,78 +461,3 @@ def test_conv1x1_nchw_x3(dev, B, HW, cout, co, oc, Cx):
 
 
 
-
-def _basic_chain_ref(x, blocks):
-    """The reference BasicBlocks (myhrnet.py:34-63) in f64: relu(bn2(conv2(relu(bn1(conv1(x))))) + x)."""
-    y = x.double()
-    for conv1, bn1, conv2, bn2 in blocks:
-        h = torch.relu(torch.nn.functional.batch_norm(
-            torch.nn.functional.conv2d(y, conv1.weight.double(), padding=1), bn1.running_mean.double(),
-            bn1.running_var.double(), bn1.weight.double(), bn1.bias.double(), eps=bn1.eps))
-        z = torch.nn.functional.batch_norm(torch.nn.functional.conv2d(h, conv2.weight.double(), padding=1),
-                                           bn2.running_mean.double(), bn2.running_var.double(), bn2.weight.double(),
-                                           bn2.bias.double(), eps=bn2.eps)
-        y = torch.relu(z + y)
-    return y
-
-
-@pytest.mark.parametrize("B,c,H,W,nblk,co", [
-    (3, 18, 30, 30, 4, 0),   # W18 branch 0 (cp 20: pad channels), (16, 2) tiles
-    (4, 36, 15, 15, 4, 4),   # branch 1, channel-offset input, (4, 5)
-    (5, 72, 8, 8, 4, 0),     # branch 2, (1, 8)
-    (6, 144, 4, 4, 4, 0),    # branch 3: one m-tile, n-tiles over the waves (3, 4)
-    (2, 36, 20, 20, 2, 0),   # config-3 sizes (S = 80 / 160): (8, 3)
-    (2, 64, 15, 15, 1, 0),   # W32 branch 1
-    (3, 20, 5, 7, 2, 0)])    # ragged map, (3, 4)
-def test_hr_chain(dev, B, c, H, W, nblk, co):
-    """krrn_hr_chain_f32 (a branch's BasicBlocks in one launch, maps in LDS) vs the f64 reference:
-    f32-level error, pad channels exactly zero, nothing written past the channel slice."""
-    from pose_estimation_amd import _lib
-    from pose_estimation_amd.runtime import P, ptr
-    g = torch.Generator().manual_seed(c * H + nblk)
-    blocks = []
-    for _ in range(nblk):
-        convs = [nn.Conv2d(c, c, 3, 1, 1, bias=False) for _ in range(2)]
-        for cv in convs:
-            with torch.no_grad():
-                cv.weight.copy_(torch.randn(cv.weight.shape, generator=g) * (1.0 / (3 * c ** 0.5)))
-        blocks.append((convs[0], _bn(c, g), convs[1], _bn(c, g)))
-    x = torch.relu(torch.randn(B, c, H, W, generator=g))
-    ref = _basic_chain_ref(x, blocks).float()
-    cp = ops.pad4(c)
-    xa = _nhwc(x, dev, cs=cp + co + 4, co=co)
-    out = ops.new_act(B, H, W, c, dev, cs=cp + 8)
-    out.t.fill_(7.0)
-    keep, wts, scs, bis = [], [], [], []
-    for conv1, bn1, conv2, bn2 in blocks:
-        for cv, bn in ((conv1, bn1), (conv2, bn2)):
-            spec = ops.make_conv(cv, bn, dev, cin_p=cp)
-            w3 = ops.chain_weights_x3(spec.wt[0], cp)
-            keep += [spec, w3]
-            wts.append(w3.data_ptr())
-            scs.append(spec.scale.data_ptr())
-            bis.append(spec.bias.data_ptr())
-    import ctypes
-    n = len(wts)
-    L = _lib.lib()
-    assert L.krrn_hr_chain_query(H, W, cp) == 0
-    _lib.check(L.krrn_hr_chain_f32(ptr(xa.t), xa.cs, xa.co, ptr(out.t), out.cs, 0, B, H, W, cp, n,
-                                   ctypes.cast((ctypes.c_void_p * n)(*wts), P),
-                                   ctypes.cast((ctypes.c_void_p * n)(*scs), P),
-                                   ctypes.cast((ctypes.c_void_p * n)(*bis), P),
-                                   P(torch.cuda.current_stream().cuda_stream)), "hr_chain")
-    torch.cuda.synchronize()
-    got = out.t[..., :c].permute(0, 3, 1, 2).cpu()
-    err = float((got.double() - ref.double()).abs().max())
-    scale = float(ref.abs().max())
-    assert err <= 2e-6 * scale * nblk, (err, scale)
-    assert torch.count_nonzero(out.t[..., c:cp]).item() == 0
-    assert torch.all(out.t[..., cp:] == 7.0)
-
-
-def test_hr_chain_rejects(dev):
-    from pose_estimation_amd import _lib
-    L = _lib.lib()
-    assert L.krrn_hr_chain_query(30, 30, 20) == 0
-    assert L.krrn_hr_chain_query(40, 40, 20) < 0     # two 40 x 40 x 20 maps exceed the LDS
-    assert L.krrn_hr_chain_query(30, 30, 18) < 0     # channels not a multiple of 4

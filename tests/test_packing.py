@@ -46,27 +46,3 @@ def test_panel_chain_layout_reconstructs_weights():
                     # three exact bf16 terms: the f32 sum is exact in f64
                     assert float(h.double() + m.double() + l_.double()) == float(W[n, k0 + e])
 
-
-def test_chain_weights_layout_reconstructs_weights():
-    """ops.chain_weights_x3: word (t, s, lane, i) of the [m h] plane and (t, s, lane, j) of the [l]
-    plane hold the split terms of W[16 t + lane % 16, 4 (4 s + lane / 16) + e] (k = tap * cp + c),
-    h + m + l == W exactly, and zero past cp output channels / 9 cp inputs."""
-    g = torch.Generator().manual_seed(1)
-    cp = 20
-    W = torch.randn(cp, 9 * cp, generator=g)
-    P = ops.chain_weights_x3(W, cp)
-    NT, S = 2, (9 * cp // 4 + 3) // 4
-    assert P.dtype == torch.int32 and P.numel() == NT * S * 64 * 6
-    mh = P[:NT * S * 64 * 4].reshape(NT, S, 64, 4)
-    lp = P[NT * S * 64 * 4:].reshape(NT, S, 64, 2)
-    for t in range(NT):
-        for s in (0, 5, S - 1):
-            for lane in (0, 3, 16, 31, 47, 63):
-                n, kq = 16 * t + lane % 16, 4 * s + lane // 16
-                for e in range(4):
-                    m = _bf16_to_f32(mh[t, s, lane, e // 2], e % 2 == 1)
-                    h = _bf16_to_f32(mh[t, s, lane, 2 + e // 2], e % 2 == 1)
-                    l = _bf16_to_f32(lp[t, s, lane, e // 2], e % 2 == 1)
-                    k = 4 * kq + e
-                    want = W[n, k] if (n < cp and k < 9 * cp) else 0.0
-                    assert float(h + m + l) == float(want), (t, s, lane, e)
