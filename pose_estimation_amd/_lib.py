@@ -12,9 +12,11 @@ import threading
 
 import torch  # noqa: F401  (loads the HIP runtime libamdhip64.so.7 before our library)
 
+from . import knobs
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # KRRN_HIP_LIB: an alternative build of the same library (kernel-variant experiments)
-LIB_PATH = os.environ.get("KRRN_HIP_LIB") or os.path.join(_HERE, "libkrrn_hip.so")
+LIB_PATH = knobs.text("KRRN_HIP_LIB") or os.path.join(_HERE, "libkrrn_hip.so")
 
 _lock = threading.Lock()
 _lib = None

@@ -150,6 +150,52 @@ __device__ inline void rodrigues(const double w0, const double w1, const double 
     }
 }
 
+// Element e = 3a + b of the same R, dR, d2R (the same D2 operations as rodrigues, one entry):
+// nine lanes build a crop's rotation side by side instead of lane 0 holding all nine D2 entries
+// (117 doubles, which went to scratch in the backward kernel).
+__device__ inline void rodrigues_elem(const double w0, const double w1, const double w2, int e, Rot& o) {
+  const D2 w[3] = {d2_var(w0, 0), d2_var(w1, 1), d2_var(w2, 2)};
+  const int a = e / 3, b = e % 3;
+  D2 m;
+  const double th2v = w0 * w0 + w1 * w1 + w2 * w2;
+  if (th2v > kKorniaEps) {
+    const D2 th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    const D2 th = d2_sqrt(th2);
+    const D2 inv = d2_inv(th + d2_const(kKorniaEps));
+    const D2 x = w[0] * inv, y = w[1] * inv, z = w[2] * inv;
+    const D2 c = d2_cos(th), s = d2_sin(th);
+    const D2 oc = d2_const(1.0) - c;
+    switch (e) {
+      case 0: m = c + x * x * oc; break;
+      case 1: m = x * y * oc - z * s; break;
+      case 2: m = y * s + x * z * oc; break;
+      case 3: m = z * s + x * y * oc; break;
+      case 4: m = c + y * y * oc; break;
+      case 5: m = -(x * s) + y * z * oc; break;
+      case 6: m = -(y * s) + x * z * oc; break;
+      case 7: m = x * s + y * z * oc; break;
+      default: m = c + z * z * oc; break;
+    }
+  } else {
+    switch (e) {
+      case 1: m = -w[2]; break;
+      case 2: m = w[1]; break;
+      case 3: m = w[2]; break;
+      case 5: m = -w[0]; break;
+      case 6: m = -w[1]; break;
+      case 7: m = w[0]; break;
+      default: m = d2_const(1.0); break;
+    }
+  }
+  o.R[a][b] = m.v;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    o.dR[j][a][b] = m.g[j];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) o.d2R[j][l][a][b] = m.h[j][l];
+  }
+}
+
 __device__ inline void matvec(const double (&A)[3][3], const double (&v)[3], double (&o)[3]) {
 #pragma unroll
   for (int a = 0; a < 3; ++a) o[a] = A[a][0] * v[0] + A[a][1] * v[1] + A[a][2] * v[2];
@@ -171,13 +217,21 @@ __device__ inline bool solve6(double (&A)[6][6], double (&b)[6], double (&x)[6])
     for (int r = c + 1; r < 6; ++r)
       if (fabs(A[r][c]) > best) { best = fabs(A[r][c]); p = r; }
     if (!(best > 0.0)) return false;
+    // row swap c <-> p as selects over the candidate rows (a branch on the pivot row let the
+    // compiler index A dynamically and put it in scratch)
 #pragma unroll
-    for (int r = 0; r < 6; ++r)
-      if (r == p && r != c) {
+    for (int r = c + 1; r < 6; ++r) {
+      const bool sw = r == p;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) { const double t = A[c][k]; A[c][k] = A[r][k]; A[r][k] = t; }
-        const double t = b[c]; b[c] = b[r]; b[r] = t;
+      for (int k = 0; k < 6; ++k) {
+        const double t = A[r][k];
+        A[r][k] = sw ? A[c][k] : t;
+        A[c][k] = sw ? t : A[c][k];
       }
+      const double t = b[r];
+      b[r] = sw ? b[c] : t;
+      b[c] = sw ? t : b[c];
+    }
 #pragma unroll
     for (int r = c + 1; r < 6; ++r) {
       const double f = A[r][c] / A[c][c];
@@ -277,7 +331,8 @@ struct CropIn {
   double K[3][3], t[3], w[3];
 };
 
-// the crop's pose, K and rotation derivatives, built by lane 0 into LDS (uniform over the wave)
+// the crop's pose, K and rotation derivatives, built into LDS (uniform over the wave): lane 0 the
+// pose and K, lanes 0-8 one rotation entry each
 __device__ inline void load_crop(const float* P6, const float* Kp, int b, CropIn& c) {
   if (threadIdx.x == 0) {
 #pragma unroll
@@ -287,8 +342,9 @@ __device__ inline void load_crop(const float* P6, const float* Kp, int b, CropIn
 #pragma unroll
       for (int e = 0; e < 3; ++e) c.K[a][e] = (double)Kp[3 * a + e];
     }
-    rodrigues(c.w[0], c.w[1], c.w[2], c.R);
   }
+  if (threadIdx.x < 9)
+    rodrigues_elem((double)P6[b * 6], (double)P6[b * 6 + 1], (double)P6[b * 6 + 2], threadIdx.x, c.R);
   __syncthreads();
 }
 
@@ -302,25 +358,34 @@ __global__ __launch_bounds__(64) void bpnp_backward_kernel(const float* __restri
   load_crop(P6, Kp, b, C);
   const float* Z = z3 + (size_t)b * z_bs;
   const float* X = x2 + (size_t)b * n * 2;
-  // pass 1: J_fy (6x6) and J_fK (6x9) summed over points
-  double Jy[6][6], JK[6][9];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-#pragma unroll
-    for (int l = 0; l < 6; ++l) Jy[j][l] = 0.0;
-#pragma unroll
-    for (int e = 0; e < 9; ++e) JK[j][e] = 0.0;
-  }
+  // pass 1: J_fy (6x6) and J_fK (6x9) summed over points. Every lane's 90 running sums live in
+  // LDS (column = lane, conflict-free 8-byte rows) instead of registers: held in VGPRs beside the
+  // point geometry they spilled 1860 B per lane to scratch. The summation order is unchanged (each
+  // lane in point order, then the wave's butterfly), so the results are bit-identical.
+  constexpr int kJ = 36 + 54;
+  __shared__ double acc[kJ][64];
+  __shared__ double red[kJ];
+#pragma unroll 1
+  for (int e = 0; e < kJ; ++e) acc[e][lane] = 0.0;
   for (int i = lane; i < n; i += 64) {
     const double z[3] = {(double)Z[3 * i], (double)Z[3 * i + 1], (double)Z[3 * i + 2]};
     const double x[2] = {(double)X[2 * i], (double)X[2 * i + 1]};
     PointGeo G;
     point_geo(C.R, C.K, C.t, z, G);
     const double r[2] = {x[0] * G.s - G.q[0], x[1] * G.s - G.q[1]};
-    // columns y_l
-#pragma unroll
+    // columns y_l (not unrolled: the fifteen columns' operands at once did not fit the register
+    // file; dq = Q_l is rebuilt from the LDS copy of R' / K, the same products as point_geo's)
+#pragma unroll 1
     for (int l = 0; l < 6; ++l) {
-      double dQ[6][3], df[6];
+      double dQ[6][3], df[6], ql[3];
+      if (l < 3) {
+        double v[3];
+        matvec(C.R.dR[l], z, v);
+        matvec(C.K, v, ql);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) ql[e] = C.K[e][l - 3];
+      }
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         if (j < 3 && l < 3) {
@@ -331,9 +396,9 @@ __global__ __launch_bounds__(64) void bpnp_backward_kernel(const float* __restri
           dQ[j][0] = dQ[j][1] = dQ[j][2] = 0.0;
         }
       }
-      dir_deriv(G, x, r, G.Q[l], dQ, df);
+      dir_deriv(G, x, r, ql, dQ, df);
 #pragma unroll
-      for (int j = 0; j < 6; ++j) Jy[j][l] += df[j];
+      for (int j = 0; j < 6; ++j) acc[j * 6 + l][lane] += df[j];
     }
     // columns K[a][e2]: dq = e_a p_e2, dQ_j = e_a (dR_j z)_e2 (j < 3) or e_a delta(e2, j-3)
 #pragma unroll
@@ -349,23 +414,22 @@ __global__ __launch_bounds__(64) void bpnp_backward_kernel(const float* __restri
         }
         dir_deriv(G, x, r, dq, dQ, df);
 #pragma unroll
-        for (int j = 0; j < 6; ++j) JK[j][3 * a + e2] += df[j];
+        for (int j = 0; j < 6; ++j) acc[36 + j * 9 + 3 * a + e2][lane] += df[j];
       }
   }
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-#pragma unroll
-    for (int l = 0; l < 6; ++l) Jy[j][l] = wave_sum(Jy[j][l]);
-#pragma unroll
-    for (int e = 0; e < 9; ++e) JK[j][e] = wave_sum(JK[j][e]);
+#pragma unroll 1
+  for (int e = 0; e < kJ; ++e) {
+    const double t = wave_sum(acc[e][lane]);
+    if (lane == 0) red[e] = t;
   }
+  __syncthreads();
   // v = -g J_fy^-1  <=>  J_fy^T v = -g
   double A[6][6], rhs[6], v[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     rhs[j] = -(double)gout[b * 6 + j];
 #pragma unroll
-    for (int l = 0; l < 6; ++l) A[j][l] = Jy[l][j];
+    for (int l = 0; l < 6; ++l) A[j][l] = red[l * 6 + j];
   }
   if (!solve6(A, rhs, v)) {
 #pragma unroll
@@ -374,7 +438,7 @@ __global__ __launch_bounds__(64) void bpnp_backward_kernel(const float* __restri
   if (lane < 9) {
     double s = 0.0;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) s += v[j] * JK[j][lane];
+    for (int j = 0; j < 6; ++j) s += v[j] * red[36 + j * 9 + lane];
     gK_part[b * 9 + lane] = s;
   }
   // pass 2: grad_x (J_fx = c s) and the per-crop grad_z

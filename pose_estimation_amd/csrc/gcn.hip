@@ -193,14 +193,9 @@ KRRN_API int krrn_knn_f32(const float* q, long long q_bs, int q_st, int nq, cons
   // lanes per query: 16 when 4 lanes would leave the grid under ~4 blocks per CU (few queries
   // per crop) AND every lane still scans >= 48 candidates (the 16-list merge is serial): the
   // pools' N/4 sampled rows against N candidates (57 -> 34 us at B = 64, N = 1000); the level-0
-  // N x N search and the short level-1 / 2 / nearest scans keep 4 (profiles/bench_knn.py;
-  // KRRN_KNN_PARTS overrides)
-  static const int force = [] {
-    const char* e = getenv("KRRN_KNN_PARTS");
-    return e ? atoi(e) : 0;
-  }();
+  // N x N search and the short level-1 / 2 / nearest scans keep 4 (profiles/bench_knn.py)
   const long long blocks4 = (long long)krrn_cdiv(nq, kKnnThreads / 4) * B;
-  const bool wide = force ? force == 16 : (blocks4 < 1024 && nc >= 16 * 48);
+  const bool wide = blocks4 < 1024 && nc >= 16 * 48;
   if (d == 3) {
     if (wide) knn_launch<3, 16>(B, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, dr, mode, out);
     else knn_launch<3, 4>(B, s, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, K, dr, mode, out);
@@ -357,7 +352,7 @@ __global__ __launch_bounds__(kGcnThreads) void gcn_conv_kernel(
 //   * __launch_bounds__(256, 4): >= 4 waves per SIMD, each with its k gather loads in flight.
 // DBG (diagnostics build only, -DKRRN_DIAG=1: krrn_gcn_debug, csrc/krrn_diag.h; surface convs only): per-point / per-block records of what the
 // block read and held in LDS, at the start and at the end of the support loop.
-template <bool HAS_Y, int KC, bool BUF = true, bool DBG = false>
+template <bool HAS_Y, int KC, bool DBG = false>
 __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
     const int* __restrict__ idx, int n, const float* __restrict__ v, long long v_bs, int v_st,
     const float* __restrict__ dn, int S, const float* __restrict__ Y, const float* __restrict__ bn_s,
@@ -482,12 +477,8 @@ __global__ __launch_bounds__(256, GCN3_WAVES) void gcn_conv3_kernel(
       asm volatile("" : "+v"(nbo));
 #pragma unroll
       for (int j = 0; j < KC; ++j) {
-        if constexpr (BUF)
-          yv[j] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(snb[nbo + j] * yrow * 4) + cbyte, s * C * 4, 0));
-        else
-          yv[j] = *reinterpret_cast<const f32x4*>(Y + (long long)b * n * yrow + (long long)snb[nbo + j] * yrow + C + c +
-                                                  s * C);
+        yv[j] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(snb[nbo + j] * yrow * 4) + cbyte, s * C * 4, 0));
       }
     }
     f32x4 w[3];
@@ -583,18 +574,7 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
   const bool wide = C >= 512;  // LP = 128 lanes per point (see the kernel comment)
   dim3 grid(krrn_cdiv(n, wide ? kGcnThreads / 128 : kGcnThreads / 32), B);
   hipStream_t s = (hipStream_t)stream;
-  // KRRN_GCN_LEGACY: 1 = the register-hoisted form for every level; 2 = only for the convs with Y;
-  // 3 = only for the surface convs (diagnostics). KRRN_GCN3_BUF=0: plain global loads of Y rows.
-  static const int legacy = [] {
-    const char* e = getenv("KRRN_GCN_LEGACY");
-    return e ? atoi(e) : 0;
-  }();
-  static const int bufload = [] {
-    const char* e = getenv("KRRN_GCN3_BUF");
-    return e ? atoi(e) : 1;
-  }();
-  const bool use3 = legacy == 0 || (legacy == 2 && !Y) || (legacy == 3 && Y);
-  if (use3 && d == 3 && C == 128 && S <= kGcnSmax && (k == 10 || k == 8) &&
+  if (d == 3 && C == 128 && S <= kGcnSmax && (k == 10 || k == 8) &&
       (long long)n * (S + 1) * C * 4 < (1LL << 31)) {
     unsigned* dbg = nullptr;
 #if KRRN_DIAG
@@ -603,28 +583,24 @@ KRRN_API int krrn_gcn_conv_f32(const int* idx, int n, int k, const float* v, lon
       dbg = g_gcn_dbg.buf + (g_gcn_dbg.count++ % g_gcn_dbg.nslots) * g_gcn_dbg.slot_words;
     }
 #endif
-#define KRRN_GCN3(HY, KC, BF) \
-  hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC, BF>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
+#define KRRN_GCN3(HY, KC) \
+  hipLaunchKernelGGL((gcn_conv3_kernel<HY, KC>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs, v_st, dn, S, Y, \
                      bn_scale, bn_bias, relu, out, o_bs, o_st, dbg)
 #if KRRN_DIAG
     if (dbg) {
       if (k == 10)
-        hipLaunchKernelGGL((gcn_conv3_kernel<false, 10, true, true>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs,
+        hipLaunchKernelGGL((gcn_conv3_kernel<false, 10, true>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs,
                            v_st, dn, S, Y, bn_scale, bn_bias, relu, out, o_bs, o_st, dbg);
       else
-        hipLaunchKernelGGL((gcn_conv3_kernel<false, 8, true, true>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs,
+        hipLaunchKernelGGL((gcn_conv3_kernel<false, 8, true>), grid, dim3(kGcnThreads), 0, s, idx, n, v, v_bs,
                            v_st, dn, S, Y, bn_scale, bn_bias, relu, out, o_bs, o_st, dbg);
       return krrn_launch_status();
     }
 #endif
     if (Y) {
-      if (bufload) {
-        if (k == 10) KRRN_GCN3(true, 10, true); else KRRN_GCN3(true, 8, true);
-      } else {
-        if (k == 10) KRRN_GCN3(true, 10, false); else KRRN_GCN3(true, 8, false);
-      }
+      if (k == 10) KRRN_GCN3(true, 10); else KRRN_GCN3(true, 8);
     } else {
-      if (k == 10) KRRN_GCN3(false, 10, true); else KRRN_GCN3(false, 8, true);
+      if (k == 10) KRRN_GCN3(false, 10); else KRRN_GCN3(false, 8);
     }
 #undef KRRN_GCN3
     return krrn_launch_status();

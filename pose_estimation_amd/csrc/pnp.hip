@@ -981,17 +981,9 @@ KRRN_API int krrn_pnp_ransac_f32(const float* xyz, int HW, const long long* choo
   float* hyp_pose = workspace;
   int* hyp_cnt = reinterpret_cast<int*>(workspace + (size_t)B * H * 12);
   // hypotheses per block: 4 (one wave) leaves no idle tail groups at H = 100 and schedules at wave
-  // granularity (occupancy is one wave per SIMD either way); 16 = the round-2 4-wave blocks
-  static const int hpb = [] {
-    const char* e = getenv("KRRN_PNP_HPB");
-    return e && atoi(e) == 16 ? 16 : 4;
-  }();
-  if (hpb == 16)
-    hipLaunchKernelGGL(pnp_hyp_kernel<16>, dim3(B, krrn_cdiv(H, 16)), dim3(256), sizeof(float) * 5 * (size_t)P, s,
-                       xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
-  else
-    hipLaunchKernelGGL(pnp_hyp_kernel<4>, dim3(B, krrn_cdiv(H, 4)), dim3(64), sizeof(float) * 5 * (size_t)P, s,
-                       xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
+  // granularity (occupancy is one wave per SIMD either way; the round-2 4-wave blocks of 16 were slower)
+  hipLaunchKernelGGL(pnp_hyp_kernel<4>, dim3(B, krrn_cdiv(H, 4)), dim3(64), sizeof(float) * 5 * (size_t)P, s,
+                     xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent, lfborder, subsets, H, thr, hyp_pose, hyp_cnt);
   hipLaunchKernelGGL(pnp_refine_kernel, dim3(B), dim3(64), 0, s, xyz, HW, choose, N, sel, P, xmap, ymap, K4, extent,
                      lfborder, H, thr, conf, hyp_pose, hyp_cnt, R, t, inliers, inlier_mask);
   return krrn_launch_status();

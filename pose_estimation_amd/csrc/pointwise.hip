@@ -328,10 +328,7 @@ KRRN_API int krrn_resize_bilinear_f32(const float* in, int B, int Hi, int Wi, in
   const long long total2 = (long long)B * Ho2 * Wo2 * (C / 4);
   // the 2x2 form for large upsamples only (the heads' 472 MB ones: 161 -> 118 us); the HRNet
   // fuse layers' small ones want the 4x more threads of the plain kernel (7.6 vs 9.0 us)
-  static const long long up_min = [] {
-    const char* e = getenv("KRRN_RESIZE_UP_MIN");
-    return e ? atoll(e) : (1LL << 21);
-  }();
+  constexpr long long up_min = 1LL << 21;
   if (Ho >= Hi && Wo >= Wi && total2 >= up_min && total2 < 0x7fffffffLL) {
     hipLaunchKernelGGL(resize_up2x2_kernel, grid1(total2), dim3(256), 0, (hipStream_t)stream, in, Hi, Wi, in_cs, in_co,
                        C / 4, out, Ho, Wo, out_cs, out_co, add, add_cs, add_co, sh, sw, align_corners, relu, Ho2, Wo2,

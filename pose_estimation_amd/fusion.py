@@ -21,8 +21,6 @@ activation.
 """
 from __future__ import annotations
 
-import os
-
 import math
 from typing import Callable, Dict, List, Optional
 
@@ -30,7 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import knobs, ops
 from .runtime import Late, Plan, add_conv, add_gemm, ptr
 
 
@@ -92,7 +90,7 @@ class FusionNetLite(nn.Module):
 
 FEAT_SID = 4  # plan stream of the materialised output concat (joined by the caller)
 # crops per chunk of the level-0 GEMM + gather-conv (0: the whole batch in one launch each)
-FUSION_CHUNK = int(os.environ.get("KRRN_FUSION_CHUNK", "0"))
+FUSION_CHUNK = knobs.integer("KRRN_FUSION_CHUNK")
 
 def level_sizes(N: int, k0: int):
     N1 = int(N / 4)

@@ -20,38 +20,29 @@ pad channels are exactly zero and the packed weights map logical -> physical cha
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Tuple
 
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import knobs, ops
 from .config import load_hrnet_spec
 from .ops import Act, pad4
 from .runtime import add_conv_group, add_gemm, add_small_group, Plan, add_conv, ptr
 
-# HRNet branch convs as per-branch chains on plan streams (KRRN_HR_GROUP=0) or as grouped
-# launches, one per block depth (KRRN_HR_GROUP=1)
-HR_GROUP = os.environ.get("KRRN_HR_GROUP", "0") == "1"
-# deconv_layer folded through the linear last_layer_2 (build_hrnet_plan)
-DECONV_FOLD = os.environ.get("KRRN_DECONV_FOLD", "1") == "1"
-# transposed convs (4 parity-class convs) as one grouped launch
-CONVT_GROUP = os.environ.get("KRRN_CONVT_GROUP", "1") == "1"
-CONVT_GROUP_TILE = int(os.environ.get("KRRN_CONVT_TILE", "8"))
-# k order of the grouped transposed convs: channel chunks of this many channels outer, taps inner
-# (krrn_conv_desc.k_chunk; 0 = tap-major)
-CONVT_KCHUNK = int(os.environ.get("KRRN_CONVT_KCHUNK", "16"))
-# narrow 3x3 stride-1 convs (the HRNet branches' BasicBlocks) on the LDS-staged direct kernel
-SMALL_CONV = os.environ.get("KRRN_SMALL_CONV", "1") == "1"
-# wide 1x1 convs as hipBLASLt GEMMs
-GEMM_1X1 = os.environ.get("KRRN_GEMM_1X1", "1") == "1"
-# fuse-layer sums opened by the identity term (no add_relu launches; _fuse_output)
-FUSE_ID_FIRST = os.environ.get("KRRN_FUSE_ID_FIRST", "1") == "1"
-# Winograd convs on the bf16 matrix cores with f32-accurate split operands (krrn_conv3x3_wino_x3_f32)
-WINO_X3 = os.environ.get("KRRN_WINO_X3", "1") == "1"
-# implicit-GEMM convs (transposed convs, stem / transitions) likewise (krrn_conv2d[_group]_x3_f32)
-CONV_X3 = os.environ.get("KRRN_CONV_X3", "1") == "1"
+# switches (pose_estimation_amd/knobs.py has each one's meaning)
+HR_GROUP = knobs.flag("KRRN_HR_GROUP")
+DECONV_FOLD = knobs.flag("KRRN_DECONV_FOLD")
+CONVT_GROUP = knobs.flag("KRRN_CONVT_GROUP")
+SMALL_CONV = knobs.flag("KRRN_SMALL_CONV")
+GEMM_1X1 = knobs.flag("KRRN_GEMM_1X1")
+FUSE_ID_FIRST = knobs.flag("KRRN_FUSE_ID_FIRST")
+WINO_X3 = knobs.flag("KRRN_WINO_X3")
+CONV_X3 = knobs.flag("KRRN_CONV_X3")
+# tile of the grouped transposed convs, and their k order: channel chunks of this many channels
+# outer, taps inner (krrn_conv_desc.k_chunk; 0 = tap-major)
+CONVT_GROUP_TILE = 8
+CONVT_KCHUNK = 16
 
 BN_MOMENTUM = 0.1
 
@@ -556,7 +547,8 @@ def build_hrnet_plan(net: HRNet, plan: Plan, x: Act) -> Tuple[Act, Act, list]:
         wa, wb = w[:L], w[L:L + Cb]
         w_eff = wa + torch.einsum("ci,cokl->iokl", w2, wb)
         w_one = torch.einsum("c,cokl->okl", b2, wb)[None]
-        folded = nn.ConvTranspose2d(L + 1, dc.out_channels, dc.kernel_size, dc.stride, dc.padding, bias=False)
+        folded = nn.utils.skip_init(nn.ConvTranspose2d, L + 1, dc.out_channels, dc.kernel_size, dc.stride, dc.padding,
+                                    bias=False)
         with torch.no_grad():
             folded.weight.copy_(torch.cat([w_eff, w_one]).float())
         x1o = Act(ycat.t, ycat.B, ycat.H, ycat.W, ycat.cs, 0, L + 1)

@@ -28,7 +28,6 @@ grow ~ B*S^2): an eval over many crop-size buckets keeps the most recently used 
 from __future__ import annotations
 
 import ctypes
-import os
 from collections import OrderedDict
 
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -36,7 +35,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import knobs, ops
 from .config import CONFIG
 from .fusion import FEAT_SID, FusionNetLite, build_fusion_plan, level_sizes
 from .hrnet import _Builder, build_hrnet, build_hrnet_plan
@@ -46,17 +45,13 @@ from .runtime import Late, Plan, add_conv, h2d, ptr
 
 # the wide head's final 1x1 conv (xyz_final, K = 128) on split-bf16 operands (f32 accuracy,
 # krrn_conv1x1_nchw_x3_f32) instead of f32 MFMAs
-NCHW_X3 = os.environ.get("KRRN_NCHW_X3", "1") == "1"
+NCHW_X3 = knobs.flag("KRRN_NCHW_X3")
 
 
-TBASE_EARLY = os.environ.get("KRRN_TBASE_EARLY", "1") == "1"
-# crops per chunk of the heads' full-resolution tail (x2 upsample + the S-px convs + final 1x1): each
-# chunk's maps (7.4 MB per crop and map at S = 120) are written and re-read through reused chunk
-# buffers while they sit in the Infinity Cache, instead of B-crop round trips through HBM (0: off)
-HEAD_CHUNK = int(os.environ.get("KRRN_HEAD_CHUNK", "0"))
+TBASE_EARLY = knobs.flag("KRRN_TBASE_EARLY")
 # KRRN.forward replays a hipGraph of its plan (captured after one serial warm-up run): the only
 # form in which the plan's side streams run concurrently (runtime.Plan); 0 = serial eager runs
-GRAPH = os.environ.get("KRRN_GRAPH", "1") == "1"
+GRAPH = knobs.flag("KRRN_GRAPH")
 
 
 class KRRNPlan:
@@ -65,10 +60,17 @@ class KRRNPlan:
     # side stream of the pose step when it is fused into the forward plan (pose_hook)
     POSE_SID = 6
     TBASE_SID = 5  # TBase conv1's level-1 half (posenet.emit_tbase_level1)
-    POSE_AT = os.environ.get("KRRN_POSE_AT", "level1")  # measured: level1 16.68, heads 16.80, level2 16.80 ms/step
+    POSE_AT = knobs.text("KRRN_POSE_AT")  # measured: level1 16.68, heads 16.80, level2 16.80 ms/step
 
     def __init__(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device, pose_hook=None,
                  pose_stream: bool = True):
+        # building a plan must not move the caller's CPU generator: the forward's pool draws (and
+        # get_pose's) follow the reference's torch.randperm sequence whether or not this call
+        # compiled a plan (a folded module's constructor initialises its weights from it)
+        with torch.random.fork_rng(devices=[]):
+            self._build(model, B, S, N, opt_pose, device, pose_hook, pose_stream)
+
+    def _build(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device, pose_hook, pose_stream):
         self.B, self.S, self.N, self.opt_pose = B, S, N, opt_pose
         cfg = model.cfg
         C = model.num_cls
@@ -202,32 +204,15 @@ class KRRNPlan:
     def _head_tail(self, bld: _Builder, x: Act, convs, final: nn.Conv2d, out: torch.Tensor, n_store: int):
         """A head's full-resolution tail (krrn.py:56-65 / 78-84): UpsamplingBilinear2d(x2) ->
         [conv3x3 + BN + ReLU] x len(convs) -> the final 1x1 (+ bias) into the NCHW map `out`, the
-        upsample folded as the first conv's input (conv_up2). With HEAD_CHUNK = c the crops run in
-        chunks of c through c-crop buffers that every chunk reuses (the same kernels per crop)."""
-        B = x.B
-        c = B if not HEAD_CHUNK or HEAD_CHUNK >= B else HEAD_CHUNK
+        upsample folded as the first conv's input (conv_up2). Running it in crop chunks through
+        reused chunk buffers (the upsampled map kept in the Infinity Cache) measured 0.8 % slower
+        (DESIGN.md section 4, round 5)."""
         spec = ops.make_conv(final, None, self.plan.device, cin_p=pad4(convs[-1][0].out_channels))
         bld.specs.append(spec)
-        if c == B:
-            h = bld.conv_up2(x, convs[0][0], convs[0][1], relu=True)
-            for conv, bn in convs[1:]:
-                h = bld.conv(h, conv, bn, relu=True)
-            self._nchw_conv(h, spec, out, n_store)
-            return
-        H, W = 2 * x.H, 2 * x.W
-        cb = _Builder(self.plan, c)
-        cb.specs = bld.specs
-        up = cb.act(H, W, x.c)
-        mids = [cb.act(H, W, conv.out_channels) for conv, _ in convs]
-        for b0 in range(0, B, c):
-            nb = min(c, B - b0)
-            xv = Act(x.t[b0:b0 + nb], nb, x.H, x.W, x.cs, x.co, x.c)
-            uv = Act(up.t[:nb], nb, H, W, up.cs, up.co, up.c)
-            cb.resize(xv, uv, align=True)
-            h = uv
-            for (conv, bn), m in zip(convs, mids):
-                h = cb.conv(h, conv, bn, out=Act(m.t[:nb], nb, H, W, m.cs, m.co, m.c), relu=True)
-            self._nchw_conv(h, spec, out[b0:b0 + nb], n_store)
+        h = bld.conv_up2(x, convs[0][0], convs[0][1], relu=True)
+        for conv, bn in convs[1:]:
+            h = bld.conv(h, conv, bn, relu=True)
+        self._nchw_conv(h, spec, out, n_store)
 
     def _nchw_conv(self, x: Act, spec, out: torch.Tensor, n_store: int):
         """The heads' final 1x1 conv + bias written NCHW (krrn.py:97-98, 80-84):
@@ -338,7 +323,7 @@ def plan_bytes(plan) -> int:
     return total
 
 
-PLAN_BUDGET = int(float(os.environ.get("KRRN_PLAN_BUDGET_GB", "48")) * (1 << 30))
+PLAN_BUDGET = int(float(knobs.text("KRRN_PLAN_BUDGET_GB")) * (1 << 30))
 
 
 class KRRN(nn.Module):

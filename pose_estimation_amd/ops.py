@@ -10,11 +10,9 @@ import ctypes
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
-import os
-
 import torch
 
-from . import _lib
+from . import _lib, knobs
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -328,8 +326,7 @@ def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:
 def wino_eligible(spec: ConvSpec, M: int) -> bool:
     """Fused Winograd for the wide stride-1 3x3 convs (>= 32 channels in and out, >= 32k output
     pixels); the narrow HRNet branches stay on the implicit GEMM (latency-bound there)."""
-    import os
-    if os.environ.get("KRRN_WINO", "1") == "0":
+    if not knobs.flag("KRRN_WINO"):
         return False
     return (spec.kind == "conv" and spec.ksize == 3 and spec.stride == 1 and spec.pad == 1
             and spec.cin_p >= 32 and spec.cout >= 32 and M >= 32768)

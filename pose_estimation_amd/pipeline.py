@@ -14,7 +14,6 @@ crop of the batch is still processed exactly once per step, with the same per-cr
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -207,9 +206,7 @@ class PipelinedPipeline:
             self.stage_a.append([(_sub_plan(kp.plan, 0, cut), kp.env)])
             self.stage_b.append([(kp.device_perm_plan, {}), (_sub_plan(kp.plan, cut, len(kp.plan.ops)), kp.env),
                                  (pt.pose, {})])
-        # stage A's stream priority (KRRN_PIPE_PRIO, e.g. -1 = high): its latency-bound chain is
-        # the one to keep moving while stage B's big grids occupy the CUs
-        self.side = torch.cuda.Stream(self.device, priority=int(os.environ.get("KRRN_PIPE_PRIO", "0")))
+        self.side = torch.cuda.Stream(self.device)
         self.graphs_a: List[Optional[torch.cuda.CUDAGraph]] = [None, None]
         self.graphs_b: List[Optional[torch.cuda.CUDAGraph]] = [None, None]
         self.h = 0

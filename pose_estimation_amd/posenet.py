@@ -12,19 +12,18 @@ conv4 + the mean over points is one reduction launch per crop.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import knobs, ops
 from .runtime import Late, Plan, add_conv, add_gemm, ptr
 
 
 # conv2 gathers h1 = ReLU(P1[nn1] + P2[nn2]) inside its operand staging (krrn_gemm_x3_gather_f32)
 # instead of a separate gather-add launch writing the 262 MB h1 (KRRN_TBASE_GATHER=0: the old form)
-TBASE_GATHER = os.environ.get("KRRN_TBASE_GATHER", "1") == "1"
+TBASE_GATHER = knobs.flag("KRRN_TBASE_GATHER")
 
 
 class TBase(nn.Module):

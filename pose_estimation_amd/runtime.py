@@ -11,13 +11,12 @@ replayed for the steady-state loop.
 from __future__ import annotations
 
 import ctypes
-import os
 from contextlib import contextmanager
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import _lib, ops
+from . import _lib, knobs, ops
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -147,15 +146,15 @@ class Sync:
 # KRRN_DIAG_DROP=name[,name...]: leave every launch of those C-ABI entry points out of new plans.
 # A what-if timing diagnostic (profiles/whatif.sh: how much the step shrinks if a kernel family
 # were free); the outputs are meaningless with it set, and nothing in the package sets it.
-_DIAG_DROP = frozenset(filter(None, os.environ.get("KRRN_DIAG_DROP", "").split(",")))
+_DIAG_DROP = frozenset(filter(None, knobs.text("KRRN_DIAG_DROP").split(",")))
 # KRRN_PLAN_STREAMS=1 (default): a plan captured into a hipGraph keeps its side streams (graph
 # branches); 0 = captured serially. KRRN_STREAMS=1 (default): the two-slot pipeline's stages and
 # concurrent micro-batches replay side by side on two streams; 0 = one after the other. Rounds 3-4
 # kept it off while two graphs side by side gave a different level-0 surface-conv output; the cause
 # was a packed-FP32 VALU result going wrong beside the split-bf16 Winograd, and the library is now
 # built without packed-FP32 ops
-PLAN_STREAMS = os.environ.get("KRRN_PLAN_STREAMS", "1") == "1"
-STREAMS = os.environ.get("KRRN_STREAMS", "1") == "1"
+PLAN_STREAMS = knobs.flag("KRRN_PLAN_STREAMS")
+STREAMS = knobs.flag("KRRN_STREAMS")
 
 
 class Plan:
@@ -284,9 +283,10 @@ TILE_SHAPES = {1: (128, 128, 16), 2: (128, 64, 16), 3: (64, 64, 16), 4: (128, 12
                6: (128, 32, 32), 7: (128, 64, 32), 8: (64, 64, 32)}
 
 
-SPLITK_TILES = int(os.environ.get("KRRN_SPLITK_TILES", "256"))  # split only launches with fewer tiles
-SPLITK_NKT = int(os.environ.get("KRRN_SPLITK_NKT", "8"))        # ... and at least this many k-tiles
-SPLITK_PER = int(os.environ.get("KRRN_SPLITK_PER", "4"))        # k-tiles per split at least
+SPLITK = knobs.flag("KRRN_SPLITK")
+SPLITK_TILES = 256  # split only launches with fewer tiles
+SPLITK_NKT = 8      # ... and at least this many k-tiles
+SPLITK_PER = 4      # k-tiles per split at least
 
 
 def conv_splits(M: int, N: int, K: int, tile: int) -> int:
@@ -297,7 +297,7 @@ def conv_splits(M: int, N: int, K: int, tile: int) -> int:
     cd = lambda a, b: (a + b - 1) // b  # noqa: E731
     tiles = cd(M, BM) * cd(N, BN)
     nkt = cd(K, BK)
-    if tiles >= SPLITK_TILES or nkt < SPLITK_NKT or N % 4 or os.environ.get("KRRN_SPLITK", "1") == "0":
+    if tiles >= SPLITK_TILES or nkt < SPLITK_NKT or N % 4 or not SPLITK:
         return 1
     return max(1, min(cd(512, tiles), nkt // SPLITK_PER, 16))
 
@@ -330,8 +330,6 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
     M = B * Hg * Wg
     K = cin_p * len(taps)
     tile_req = tile
-    if tile is None and tag and os.environ.get(f"KRRN_TILE_{tag.upper()}"):  # tile-menu experiments
-        tile = int(os.environ[f"KRRN_TILE_{tag.upper()}"])
     tile = conv_tile(M, N, K, nchw) if tile is None else tile
     if splits is None:
         splits = 1 if nchw else conv_splits(M, N, K, tile)
@@ -359,7 +357,7 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
              meta=dict(kernel=kname, flops=flops, tag=tag, M=M, N=N, K=K, splits=splits))
 
 
-GROUP_TILE = int(os.environ.get("KRRN_GROUP_TILE", "6"))
+GROUP_TILE = 6
 
 
 class SmallDesc(ctypes.Structure):
@@ -437,17 +435,17 @@ def add_conv_group(plan: Plan, problems: List[dict], tile: int = None, tag: str 
     plan.add("krrn_conv2d_group_x3_f32" if x3 else "krrn_conv2d_group_f32", ctypes.cast(arr, P), n, tile, meta=meta)
 
 
-BLAS = os.environ.get("KRRN_BLAS", "1") == "1"
+BLAS = knobs.flag("KRRN_BLAS")
 BLAS_MAX_WS = 64 << 20
 # plain GEMMs with K >= GEMM_X3_MINK on gemm_x3.hip (split-bf16), the rest on hipBLASLt: measured
 # (profiles/bench_gemm.py, MI355X) 10-18 % faster at K = 256..1024, 10 % slower at K = 128 (the
 # level-0 GCN GEMMs: 198 vs 180 us, output-write-bound) and slower at layer1's K = 64 (all
 # eligible GEMMs on gemm_x3: 1.98 vs 1.77 ms of GEMMs per step)
-GEMM_X3 = os.environ.get("KRRN_GEMM_X3", "1") == "1"
+GEMM_X3 = knobs.flag("KRRN_GEMM_X3")
 # short-K GEMMs (K = 64 / 128, N % 32 == 0, one row group) on the A-stationary split-bf16 kernel
 # (gemm_panel.hip): the level-0 / level-1 GCN GEMMs, whose 262 MB output makes them write streams
-GEMM_PANEL = os.environ.get("KRRN_GEMM_PANEL", "1") == "1"
-GEMM_X3_MINK = int(os.environ.get("KRRN_GEMM_X3_MINK", "256"))
+GEMM_PANEL = knobs.flag("KRRN_GEMM_PANEL")
+GEMM_X3_MINK = 256
 
 
 class _BlasPlan:

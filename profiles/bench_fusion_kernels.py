@@ -3,7 +3,7 @@ the K = 128 GCN GEMMs (krrn_gemm_panel_x3_f32 per column split, krrn_gemm_x3_f32
 torch.mm) and the gather-convs (krrn_gcn_conv_f32: Conv_surface and Conv_layer, level 0 and 1).
 Prints one JSON line per measurement (us per launch, GB/s of the launch's compulsory bytes).
 
-usage (GPU box): python3 profiles/bench_fusion_kernels.py   (KRRN_GCN_LEGACY=1: the old gather-conv)
+usage (GPU box): python3 profiles/bench_fusion_kernels.py
 """
 import json
 import os
@@ -91,5 +91,5 @@ for level, n in ((0, N), (1, N // 4)):
                                            ptr(bb) if has_y else P(0), 1, ptr(out), n * C, C, B, st), "gcn")
         us = ev_time(run)
         byts = 4.0 * B * n * (C + ((S + 1) * C if has_y else 0))
-        emit(kernel="gcn_conv", legacy=os.environ.get("KRRN_GCN_LEGACY", "0"), level=level, has_y=has_y,
+        emit(kernel="gcn_conv", level=level, has_y=has_y,
              us=round(us, 2), GBs=round(byts / us / 1e3, 1))

@@ -1,6 +1,7 @@
 """Micro-bench: krrn_knn_f32 on the fusion's shapes (B = 64, N = 1000), 4 vs 16 lanes per query
-(KRRN_KNN_PARTS is read once per process: run with PARTS=4 and PARTS=16 in turn); prints a checksum
-of the indices so both runs can be compared for equality."""
+(the lanes-per-query rule is fixed in gcn.hip since round 5: build a variant library with the other
+choice and point KRRN_HIP_LIB at it, profiles/build_variant.sh); prints a checksum of the indices
+so both runs can be compared for equality."""
 import os
 import sys
 

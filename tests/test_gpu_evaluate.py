@@ -25,6 +25,56 @@ def test_eval_epoch_counts(dev):
     assert 0.0 <= res["auc_all"] <= 100.0
 
 
+def test_eval_records_overlap_matches_serial(dev):
+    """eval_records builds batch j+1's inputs on a side stream during batch j's forward and reads the
+    model's output views in place: every record equals the plain serial loop's (fresh outputs, one
+    stream), with the host and device RNG streams reset to the same state before each run."""
+    import numpy as np
+    from pose_estimation_amd import pose as kpose
+    from pose_estimation_amd.evaluate import REC, _R, _batches, eval_records
+    from pose_estimation_amd.metric import add_metric, rt_errors
+    ds = PoseDataset("test", 500, False, None, 0.0, 8, cls_type="all", num_frames=14,
+                     sizes=[80, 120, 80, 120, 80, 160, 80])
+    m = KRRN(cfg=make_config(num_cls=len(ds.objlist), backbone="w18"))
+    init_weights(m, 0)
+    m = m.to(dev).eval()
+    buckets = {}
+    for i in range(len(ds)):
+        buckets.setdefault(ds.crop_size(i), []).append(i)
+    metric = Metric(ds.sym_obj)
+
+    def reset():
+        torch.manual_seed(123)
+        kpose._seeds.clear()
+        ds._calls = 0
+
+    reset()
+    got = eval_records(m, ds, buckets, 3, dev, with_loss=False).numpy()
+    reset()
+    rows = []
+    with torch.no_grad():
+        for S, idx in _batches(buckets, 3):
+            d = ds.batch(idx, dev)
+            pred = m(d["img_croped"], d["cloud"], d["choose"], d["cls_id"])
+            B = len(idx)
+            br, bt = kpose.get_pose(pred, d)
+            pt = pred["pred_t"].reshape(B, 3)
+            add_b = add_metric(br, bt.reshape(B, 3), d["model_points"], d["target"], d["cls_id"], metric.sys)
+            add_f = add_metric(br, pt, d["model_points"], d["target"], d["cls_id"], metric.sys)
+            rec = np.zeros((B, len(REC)))
+            rec[:, _R["crop"]] = idx
+            rec[:, _R["cls"]] = d["cls_id"].reshape(B).cpu().numpy()
+            rec[:, _R["valid"]] = 1.0
+            rec[:, _R["add_b"]] = add_b.cpu().numpy()
+            rec[:, _R["r_b"]], rec[:, _R["t_b"]] = rt_errors(br, bt, d["target_r"], d["target_t"])
+            rec[:, _R["add_f"]] = add_f.cpu().numpy()
+            rec[:, _R["r_f"]], rec[:, _R["t_f"]] = rt_errors(br, pt, d["target_r"], d["target_t"])
+            rows.append(rec)
+    want = np.concatenate(rows)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want), np.abs(got - want).max(0)
+
+
 def test_cal_dis_gt_pose_is_zero(dev):
     ds = PoseDataset("test", 500, False, None, 0.0, 8, cls_type="all", num_frames=9, sizes=[80])
     data = ds.batch(list(range(len(ds))), dev)

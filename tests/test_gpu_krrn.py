@@ -274,3 +274,37 @@ def test_fresh_outputs_and_plan_lru(dev):
     torch.cuda.synchronize()
     assert len(m._plans) <= 3
     assert list(m._plans)[-1][1] == 40  # the most recent shape is cached
+
+
+def test_plan_build_keeps_the_cpu_generator(dev):
+    """The pool draws follow the reference's torch.randperm sequence on the CPU generator whether or
+    not a call compiled a plan: a first call (plan build + serial run), the second (graph capture) and
+    a cached replay each move the generator by exactly the forward's own five draws, so the same seed
+    gives the same pred_t on a fresh model and on a warm one."""
+    N = 256
+    d = make_batch(2, 80, N, seed=3)
+    args = (d["img_croped"].to(dev), d["cloud"].to(dev), d["choose"].to(dev), d["cls_id"].to(dev))
+
+    def model():
+        m = KRRN(cfg=make_config(num_cls=1, backbone="w18"))
+        init_weights(m, 0)
+        return m.to(dev).eval()
+
+    def draws():  # the generator after the forward's five draws alone
+        for n, k in ((N, N // 4),) * 4 + ((N // 4, N // 16),):
+            torch.randperm(n)[:k]
+        return torch.get_rng_state()
+
+    warm = model()
+    for _ in range(3):
+        warm(*args)
+    fresh = model()
+    outs = []
+    for m in (fresh, fresh, fresh, warm):
+        torch.manual_seed(77)
+        want = (torch.manual_seed(77), draws())[1]
+        torch.manual_seed(77)
+        outs.append(m(*args)["pred_t"].cpu())
+        assert torch.equal(torch.get_rng_state(), want)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
