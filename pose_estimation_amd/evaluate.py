@@ -60,16 +60,21 @@ def eval_records(model: KRRN, dataset: PoseDataset, indices: Dict[int, List[int]
     """Run the eval path over {S: [crop indices]} in batches of <= bs; returns f64 [n, len(REC)]
     (rows in the order evaluated). Every batch's inputs, forward, pose and ADD(-S) are queued on
     the device without a host round trip; the per-crop records are read back once at the end (the
-    same numbers as a per-batch read-back, without a stall per batch)."""
+    same numbers as a per-batch read-back, without a stall per batch).
+
+    Three streams: batch j+1's inputs are built on one side stream while batch j's forward runs on
+    the caller's stream (fresh tensors from resident frames), and batch j's PnP-RANSAC + ADD(-S)
+    run on another beside batch j+1's forward (one workgroup per crop: latency-bound launches that
+    fill the CUs the forward leaves idle). The pose reads a copy of the forward's 3-channel xyz map
+    (the plan's buffer is rewritten by the next forward of the same shape). Host draws keep the
+    serial order: forward j's pool perms, then get_pose j's point subsets, then forward j+1's."""
     metric = Metric(dataset.sym_obj)
     pending = []
     batches = list(_batches(indices, bs))
     device = torch.device(device)
     main = torch.cuda.current_stream(device)
-    # batch j+1's inputs are built on a side stream while batch j's forward runs (they share nothing:
-    # fresh tensors from resident frames); the forward, the pose and the metric stay in order on the
-    # caller's stream, so the model's output views may be read in place until the next forward
-    side = torch.cuda.Stream(device)
+    side = torch.cuda.Stream(device)   # inputs
+    pstr = torch.cuda.Stream(device)   # pose + metric
 
     def build(j):
         side.wait_stream(main)  # the inputs' pinned staging and allocations follow earlier work
@@ -88,6 +93,7 @@ def eval_records(model: KRRN, dataset: PoseDataset, indices: Dict[int, List[int]
             main.wait_event(ev)
             for v in data.values():
                 v.record_stream(main)
+                v.record_stream(pstr)
             if j + 1 < len(batches):
                 nxt = build(j + 1)
             pred = model(data["img_croped"], data["cloud"], data["choose"], data["cls_id"], opt_pose=opt_pose)
@@ -95,18 +101,33 @@ def eval_records(model: KRRN, dataset: PoseDataset, indices: Dict[int, List[int]
             lc = None
             if with_loss and "xyz" in data and "multi_cls_mask" in data:
                 lc = map_losses(pred, data, per_crop=True)  # [B, 8]: xyz, normal, region, mask, counts
-            base_r, base_t = get_pose(pred, data)
-            add_b = add_metric(base_r, base_t.reshape(B, 3), data["model_points"], data["target"], data["cls_id"],
-                               metric.sys)
-            add_f = pred_t = None
-            if opt_pose:
-                # reg = final = (PnP R, TBase t) (trainer.py:198-201); a copy: the view is the plan's buffer
-                pred_t = pred["pred_t"].reshape(B, 3).clone()
-                add_f = add_metric(base_r, pred_t, data["model_points"], data["target"], data["cls_id"], metric.sys)
+            # copies of what the pose step reads from the plan's output buffers
+            xyz = pred["xyz"].clone()
+            pred_t = pred["pred_t"].reshape(B, 3).clone() if opt_pose else None
+            done = torch.cuda.Event()
+            done.record(main)
+            pstr.wait_event(done)
+            xyz.record_stream(pstr)
+            if pred_t is not None:
+                pred_t.record_stream(pstr)
+            with torch.cuda.stream(pstr):
+                base_r, base_t = get_pose({"xyz": xyz}, data)
+                add_b = add_metric(base_r, base_t.reshape(B, 3), data["model_points"], data["target"],
+                                   data["cls_id"], metric.sys)
+                add_f = None
+                if opt_pose:
+                    # reg = final = (PnP R, TBase t) (trainer.py:198-201)
+                    add_f = add_metric(base_r, pred_t, data["model_points"], data["target"], data["cls_id"],
+                                       metric.sys)
             pending.append((idx, data["cls_id"], data["target_r"], data["target_t"], base_r, base_t, pred_t, add_b,
                             add_f, lc))
     finally:
         model.return_views = views
+    main.wait_stream(pstr)
+    for p in pending:  # made on the pose stream, read back on the caller's
+        for t in (p[4], p[5], p[7], p[8]):
+            if t is not None:
+                t.record_stream(main)
     if not pending:
         return torch.zeros((0, len(REC)), dtype=torch.float64)
     # one read-back and one vectorised host pass for the whole epoch: per batch, the rotation /
@@ -139,44 +160,49 @@ def fold_records(records: torch.Tensor, objlist: Sequence[int], diameter: Sequen
                  metric: Metric) -> Dict[str, object]:
     """The reference's per-object bookkeeping (trainer.py:165-250) over per-crop records, in global
     crop order (independent of how crops were batched or sharded)."""
-    rec = records[records[:, _R["valid"]] > 0]
-    rec = rec[torch.argsort(rec[:, _R["crop"]], stable=True)].numpy()
+    rec = records.numpy() if isinstance(records, torch.Tensor) else np.asarray(records)
+    rec = rec[rec[:, _R["valid"]] > 0]
+    rec = rec[np.argsort(rec[:, _R["crop"]], kind="stable")]
     result = {k: {o: 0.0 for o in objlist} for k in _KEYS}
+    cls = rec[:, _R["cls"]].astype(np.int64)
+    col = lambda k: rec[:, _R[k]]  # noqa: E731
+
+    def seq_sum(x):  # the reference's running `+=` in crop order (np.cumsum adds sequentially)
+        return float(np.cumsum(x)[-1]) if len(x) else 0.0
+
+    # first-appearance order of the objects, as the reference's dict of ADD lists fills
+    order = [int(c) for c in dict.fromkeys(cls.tolist())]
     adds: Dict[int, List[float]] = {}
-    test_dis = 0.0
-    for row in rec:
-        cls = int(row[_R["cls"]])
-        obj = objlist[cls]
-        dia = diameter[cls]
-        result["all_num"][obj] += 1
-        result["obj_num"][obj] += 1
-        ab, rb, tb = row[_R["add_b"]], row[_R["r_b"]], row[_R["t_b"]]
-        result["dis_base_rt"][obj] += ab
-        result["dis_base_r"][obj] += rb
-        result["dis_base_t"][obj] += tb
-        result["succ_base_rt"][obj] += ab < 0.1 * dia
-        result["succ_base_r"][obj] += rb < ROT_THR_DEG
-        result["succ_base_t"][obj] += tb < TRANS_THR_M
-        result["dis_xyz"][obj] += row[_R["l_xyz"]]
-        result["dis_mask"][obj] += row[_R["l_mask"]]
-        result["dis_normal"][obj] += row[_R["l_normal"]]
+    for c in order:
+        obj, dia = objlist[c], diameter[c]
+        sel = cls == c
+        n = float(sel.sum())
+        result["all_num"][obj] = result["obj_num"][obj] = n
+        ab, rb, tb = col("add_b")[sel], col("r_b")[sel], col("t_b")[sel]
+        result["dis_base_rt"][obj] = seq_sum(ab)
+        result["dis_base_r"][obj] = seq_sum(rb)
+        result["dis_base_t"][obj] = seq_sum(tb)
+        result["succ_base_rt"][obj] = float((ab < 0.1 * dia).sum())
+        result["succ_base_r"][obj] = float((rb < ROT_THR_DEG).sum())
+        result["succ_base_t"][obj] = float((tb < TRANS_THR_M).sum())
+        result["dis_xyz"][obj] = seq_sum(col("l_xyz")[sel])
+        result["dis_mask"][obj] = seq_sum(col("l_mask")[sel])
+        result["dis_normal"][obj] = seq_sum(col("l_normal")[sel])
         if opt_pose:
-            af, rf, tf = row[_R["add_f"]], row[_R["r_f"]], row[_R["t_f"]]
+            af, rf, tf = col("add_f")[sel], col("r_f")[sel], col("t_f")[sel]
             for k in ("reg", "final"):
-                result[f"dis_{k}_rt"][obj] += af
-                result[f"dis_{k}_r"][obj] += rf
-                result[f"dis_{k}_t"][obj] += tf
-                result[f"succ_{k}_rt"][obj] += af < 0.1 * dia
-                result[f"succ_{k}_r"][obj] += rf < ROT_THR_DEG
-                result[f"succ_{k}_t"][obj] += tf < TRANS_THR_M
-            test_dis += af
-            adds.setdefault(obj, []).append(float(af))
+                result[f"dis_{k}_rt"][obj] = seq_sum(af)
+                result[f"dis_{k}_r"][obj] = seq_sum(rf)
+                result[f"dis_{k}_t"][obj] = seq_sum(tf)
+                result[f"succ_{k}_rt"][obj] = float((af < 0.1 * dia).sum())
+                result[f"succ_{k}_r"][obj] = float((rf < ROT_THR_DEG).sum())
+                result[f"succ_{k}_t"][obj] = float((tf < TRANS_THR_M).sum())
+            adds[obj] = af.tolist()
         else:
-            test_dis += ab
-            adds.setdefault(obj, []).append(float(ab))
+            adds[obj] = ab.tolist()
     out = copy.copy(result)
     out["test_count"] = int(len(rec))
-    out["test_dis"] = test_dis / max(len(rec), 1)
+    out["test_dis"] = seq_sum(col("add_f") if opt_pose else col("add_b")) / max(len(rec), 1)
     out["auc"] = {o: metric.cal_auc(v) for o, v in adds.items()}
     out["auc_all"] = metric.cal_auc([a for v in adds.values() for a in v]) if adds else 0.0
     return out

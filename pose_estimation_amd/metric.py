@@ -98,8 +98,8 @@ class Metric:
         prec = prec[idx]
         mrec = np.array([0.0] + list(rec) + [0.1])
         mpre = np.array([0.0] + list(prec) + [prec[-1]])
-        for i in range(1, prec.shape[0]):
-            mpre[i] = max(mpre[i], mpre[i - 1])
+        n = prec.shape[0]  # the running max over mpre[1 .. n-1] (metric.py:61-62), as one scan
+        mpre[:n] = np.maximum.accumulate(mpre[:n])
         i = np.where(mrec[1:] != mrec[0:-1])[0] + 1
         return np.sum((mrec[i] - mrec[i - 1]) * mpre[i]) * 10
 
