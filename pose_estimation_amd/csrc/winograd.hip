@@ -344,11 +344,15 @@ __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a)
 // (m l, l m, l l) are below 2^-23 |a b|, the size of the f32 MFMA's own product rounding, and
 // everything accumulates in f32 (profiles/bench_wino_x3.py: RMS error vs f64 2.8e-7 against the
 // f32 kernel's 3.0e-7).
-// Register chains, no copies but one: a lane's 8 bf16 of an MFMA operand are 2 term kinds x its 4
-// channels (k = 8 half + i pairs A and B element i of the same lane), so with the A chain
-// [V_h V_h V_m V_l] (4 x 2 registers) and the B chain [U_m U_h U_l] (one b128 of plane U_mh + one
-// b64 of plane U_l, 6 registers) the three MFMAs are
-//   A[0:3] x B[2:5] = hh + hl,   A[2:5] x B[0:3] = hm + mh,   A[4:7] x B[0:3] = mm + lh.
+// Register chains, no copies: a lane's 8 bf16 of an MFMA operand are 2 term kinds x its 4 channels
+// (k = 8 half + i pairs A and B element i of the same lane), so with the A chain [V_m V_h V_l] and
+// the B chain [U_m U_h U_l] (one b128 of plane U_mh + one b64 of plane U_l), 6 registers each, the
+// three MFMAs are
+//   A[0:3] x B[0:3] = mm + hh,   A[0:3] x B[2:5] = mh + hl,   A[2:5] x B[0:3] = hm + lh.
+// An empty asm statement with each chain as a "+v" operand pins it to one 6-register tuple, so the
+// operand slices are sub-registers and the weight loads land in the tuple directly. Round 4's A
+// chain [V_h V_h V_m V_l] needed h twice, and LLVM rebuilt the overlapping slices with 40 register
+// copies per wave and chunk (194 -> 154 VALU instructions in the loop, 250 -> 234 VGPRs).
 // V is split in registers (v_cvt_pk_bf16_f32, RNE); U is split on the host (ops.wino_weights_x3).
 // Weight addresses: a per-lane voffset per n-block and the chunk / component part in soffset
 // (SALU); a wave reloads component v's weights for the next chunk as soon as its MFMAs have
@@ -375,17 +379,19 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
 __device__ __forceinline__ float bf_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
 __device__ __forceinline__ float bf_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xFFFF0000u); }
 
-// x (4 channels) -> the A chain [x_h x_h x_m x_l] as packed bf16 pairs
-__device__ __forceinline__ u32x8 split3_chain(const f32x4 x) {
+typedef unsigned u32x6 __attribute__((ext_vector_type(6)));
+
+// x (4 channels) -> the A chain [x_m x_h x_l] as packed bf16 pairs
+__device__ __forceinline__ u32x6 split3_chain(const f32x4 x) {
   const unsigned h0 = pk_bf16(x[0], x[1]), h1 = pk_bf16(x[2], x[3]);
   const float r0 = x[0] - bf_lo(h0), r1 = x[1] - bf_hi(h0);
   const float r2 = x[2] - bf_lo(h1), r3 = x[3] - bf_hi(h1);
   const unsigned m0 = pk_bf16(r0, r1), m1 = pk_bf16(r2, r3);
   const unsigned l0 = pk_bf16(r0 - bf_lo(m0), r1 - bf_hi(m0)), l1 = pk_bf16(r2 - bf_lo(m1), r3 - bf_hi(m1));
-  return u32x8{h0, h1, h0, h1, m0, m1, l0, l1};
+  return u32x6{m0, m1, h0, h1, l0, l1};
 }
 
-__device__ __forceinline__ bf16x8 sub4(const u32x8& c, int o) {
+__device__ __forceinline__ bf16x8 sub4(const u32x6& c, int o) {
   return __builtin_bit_cast(bf16x8, u32x4{c[o], c[o + 1], c[o + 2], c[o + 3]});
 }
 
@@ -520,13 +526,15 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
     make_v(smem + (ck % 3) * kRSlot, V);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const u32x8 ac = split3_chain(V[v]);
+      u32x6 ac = split3_chain(V[v]);
+      asm volatile("" : "+v"(ac));  // one register tuple: the MFMA operands are its sub-registers
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) {
-        const u32x8 bc = {wmh[v][j][0], wmh[v][j][1], wmh[v][j][2], wmh[v][j][3], wl[v][j][0], wl[v][j][1], 0u, 0u};
-        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 2), acc[v][j], 0, 0, 0);
-        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 2), sub4(bc, 0), acc[v][j], 0, 0, 0);
-        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 4), sub4(bc, 0), acc[v][j], 0, 0, 0);
+        u32x6 bc = {wmh[v][j][0], wmh[v][j][1], wmh[v][j][2], wmh[v][j][3], wl[v][j][0], wl[v][j][1]};
+        asm volatile("" : "+v"(bc));
+        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 0), acc[v][j], 0, 0, 0);  // mm + hh
+        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 2), acc[v][j], 0, 0, 0);  // mh + hl
+        acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 2), sub4(bc, 0), acc[v][j], 0, 0, 0);  // hm + lh
       }
       load_wv(ck + 1, v);
       // keep the reload here (hipcc otherwise sinks every weight load below all the MFMAs)
