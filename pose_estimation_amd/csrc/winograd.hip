@@ -526,15 +526,24 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
     make_v(smem + (ck % 3) * kRSlot, V);
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
+#if KRRN_WINO_EXP == 8  // timing experiment: no split (V's bits as the operand chain)
+      u32x6 ac = {__float_as_uint(V[v][0]), __float_as_uint(V[v][1]), __float_as_uint(V[v][2]),
+                  __float_as_uint(V[v][3]), __float_as_uint(V[v][0]), __float_as_uint(V[v][1])};
+#else
       u32x6 ac = split3_chain(V[v]);
+#endif
       asm volatile("" : "+v"(ac));  // one register tuple: the MFMA operands are its sub-registers
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) {
         u32x6 bc = {wmh[v][j][0], wmh[v][j][1], wmh[v][j][2], wmh[v][j][3], wl[v][j][0], wl[v][j][1]};
         asm volatile("" : "+v"(bc));
+#if KRRN_WINO_EXP == 7  // timing experiment: no MFMAs (operands still formed and loaded)
+        acc[v][j][0] += __uint_as_float(ac[0] ^ ac[4] ^ bc[0] ^ bc[4]);
+#else
         acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 0), acc[v][j], 0, 0, 0);  // mm + hh
         acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 2), acc[v][j], 0, 0, 0);  // mh + hl
         acc[v][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 2), sub4(bc, 0), acc[v][j], 0, 0, 0);  // hm + lh
+#endif
       }
       load_wv(ck + 1, v);
       // keep the reload here (hipcc otherwise sinks every weight load below all the MFMAs)
@@ -542,8 +551,19 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
     }
     store_raw((ck + 2) % 3, raw);
     load_raw(ck + 3, raw);
+#if KRRN_WINO_EXP != 10  // timing experiment 10: no barrier per chunk (results wrong)
     __syncthreads();
+#endif
   }
+#if KRRN_WINO_EXP == 11  // timing experiment: one store per lane instead of the epilogue
+  float sum = 0.f;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) sum += acc[x][j][0] + acc[x][j][15];
+  if (sum == 12345.f) a.out[tid] = sum;
+  return;
+#endif
   wino_epi_put(smem, acc);
   __syncthreads();
   wino_epi_finish2d(a, smem, b, ty0, tx0, n0);
