@@ -289,12 +289,16 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
         const unsigned* p = As + (wm * C::WTM + i * 32 + frow) * PX + 8 * q;
         const cg_u32x4 lo = *reinterpret_cast<const cg_u32x4*>(p), hi = *reinterpret_cast<const cg_u32x4*>(p + 4);
         af[i] = cg_u32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        // one 8-register tuple: both LDS reads land in it and the MFMA operands are its
+        // sub-registers (LLVM otherwise rebuilt the overlapping slices with register copies)
+        asm volatile("" : "+v"(af[i]));
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const unsigned* p = Bs + (wn * C::WTN + j * 32 + frow) * PX + 8 * q;
         const cg_u32x4 lo = *reinterpret_cast<const cg_u32x4*>(p), hi = *reinterpret_cast<const cg_u32x4*>(p + 4);
         bf[j] = cg_u32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        asm volatile("" : "+v"(bf[j]));
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
