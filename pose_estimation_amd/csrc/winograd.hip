@@ -129,23 +129,25 @@ static_assert(2 * (kRC - 1) + 1 + (kRC - 1) / 2 < kRowSlots && (kRowSlots % 8) =
 static_assert((kRR - 1) * kRowSlots + 2 * (kRC - 1) + 1 + (kRC - 1) / 2 < kRDummy, "padded ring slot fits");
 static_assert(4 * 2 * kWT * kSP >= 3 * kRSlot, "ring fits in the epilogue's LDS");
 
-// epilogue finish for a 2-D tile block: tile tl -> (ty, tx) = (tl / kGX, tl % kGX)
+// epilogue finish for a 2-D tile block of WT tiles, GX per row: tile tl -> (ty, tx) = (tl / GX, tl % GX);
+// smem holds (c0, c1) as [u][q][tile][n] with pitch kSP
+template <int WT = kWT, int GX = kGX>
 __device__ __forceinline__ void wino_epi_finish2d(const WinoArgs& a, const float* smem, int b, int ty0, int tx0,
                                                   int n0) {
-  constexpr int kNP = kWT * kN4 / 256;
+  constexpr int kNP = WT * kN4 / 256;
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < kNP; ++i) {
     const int pr = tid + 256 * i;
     const int n4 = pr % kN4, tl = pr / kN4;
     const int n = n0 + 4 * n4;
-    const int ty = ty0 + tl / kGX, tx = tx0 + tl % kGX;
+    const int ty = ty0 + tl / GX, tx = tx0 + tl % GX;
     if (ty >= a.Ht || tx >= a.Wt || n >= a.n_store) continue;
     f32x4 c[4][2];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) c[u][q] = *reinterpret_cast<const f32x4*>(smem + ((u * 2 + q) * kWT + tl) * kSP + 4 * n4);
+      for (int q = 0; q < 2; ++q) c[u][q] = *reinterpret_cast<const f32x4*>(smem + ((u * 2 + q) * WT + tl) * kSP + 4 * n4);
     f32x4 y[4];
     y[0] = c[0][0] + c[1][0] + c[2][0];
     y[1] = c[0][1] + c[1][1] + c[2][1];
