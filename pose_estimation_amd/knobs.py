@@ -44,7 +44,8 @@ KNOBS: Dict[str, Tuple[Optional[str], str]] = {
     "KRRN_TBASE_GATHER": ("1", "TBase conv1 / conv2 by linearity on the fusion's level rows (gathered "
                                "GEMM); 0 = on the materialised 1280-wide concat"),
     "KRRN_POSE_AT": ("level1", "where the fused pose step forks off the forward plan: level1 / level2 / heads"),
-    "KRRN_FUSION_CHUNK": ("0", "crops per chunk of the level-0 GCN GEMM + gather-conv (0 = whole batch)"),
+    "KRRN_FUSION_CHUNK": ("16", "crops per chunk of the level-0 GCN GEMM + gather-conv, through a chunk-sized "
+                                "Y buffer per branch (0 = the whole batch at once; same results)"),
 }
 
 

@@ -59,6 +59,6 @@ def test_defaults_are_the_shipped_configuration(monkeypatch):
     for k in knobs.KNOBS:
         monkeypatch.delenv(k, raising=False)
     assert knobs.flag("KRRN_WINO_X3") and knobs.flag("KRRN_GRAPH") and not knobs.flag("KRRN_HR_GROUP")
-    assert knobs.integer("KRRN_FUSION_CHUNK") == 0 and knobs.text("KRRN_HIP_LIB") is None
+    assert knobs.integer("KRRN_FUSION_CHUNK") == 16 and knobs.text("KRRN_HIP_LIB") is None
     monkeypatch.setenv("KRRN_HR_GROUP", "1")
     assert knobs.flag("KRRN_HR_GROUP")
