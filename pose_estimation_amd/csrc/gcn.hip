@@ -13,7 +13,6 @@
 //   krrn_pool_max_f32   Pool_layer's max over the 4 neighbours (gcn3d.py:233-236), evaluated
 //                       only at the randperm-sampled rows that the reference keeps (:238-241).
 #include <math.h>
-#include <stdlib.h>
 
 #include "krrn_common.h"
 

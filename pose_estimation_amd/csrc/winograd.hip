@@ -41,7 +41,6 @@
 // wave groups (1.95 ms), LDS-DMA weights (1.49 ms).
 #include "krrn_common.h"
 
-#include <cstdlib>
 
 namespace {
 
