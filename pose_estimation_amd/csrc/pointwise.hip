@@ -6,7 +6,6 @@
 // (posenet.py:76-80 + krrn.py:153).
 #include <math.h>
 
-
 #include "krrn_common.h"
 
 namespace {

@@ -41,7 +41,6 @@
 // wave groups (1.95 ms), LDS-DMA weights (1.49 ms).
 #include "krrn_common.h"
 
-
 namespace {
 
 constexpr int kWT = 32;       // tiles per block
