@@ -76,6 +76,7 @@ struct ConvArgs {
   int kchunk;
   unsigned kc_magic;  // ceil(2^32 / (Q * ntaps))
   unsigned q_magic;   // ceil(2^32 / Q)
+  int vec;  // NHWC epilogue in float4 channel runs (every operand it touches is 16-B aligned)
 };
 
 template <int BM, int BN, int BK, int WGM>
@@ -400,6 +401,51 @@ __device__ __forceinline__ void conv_tile(const ConvArgs& a, const int bid, cons
     s_b2[r] = m / a.b2_div;
   }
   __syncthreads();
+  if constexpr (!NCHW) {
+    if (a.vec) {
+      // each 32x32 accumulator tile goes through a per-wave LDS square ([row][n], pitch 32: the
+      // ds_write_b32 halves and the ds_read_b128 lane groups are conflict-free) and leaves as float4
+      // channel runs: 4 store instructions per lane and tile instead of 16 scalar ones
+      static_assert(3 * BM + 4 * 1024 <= 2 * (A_FLOATS + B_FLOATS), "epilogue square does not fit");
+      float* sq = smem + 3 * BM + wave * 1024;
+      const int rq = lane >> 3, cq = 4 * (lane & 7);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sq[((r & 3) + 8 * (r >> 2) + 4 * fh) * 32 + frow] = acc[i][j][r];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          f32x4 v[4];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) v[p] = *reinterpret_cast<const f32x4*>(sq + (rq + 8 * p) * 32 + cq);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const int n = n0 + wn * C::WTN + j * 32 + cq;
+          if (n >= a.n_store) continue;  // n_store is a multiple of 4
+          const f32x4 sc = a.scale ? *reinterpret_cast<const f32x4*>(a.scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+          const f32x4 bi = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const int row = wm * C::WTM + i * 32 + rq + 8 * p;
+            if (m0 + row >= a.M) continue;
+            const size_t pix = (size_t)s_b[row] * HWo + s_sp[row];
+            f32x4 o = v[p] * sc + bi;
+            if (a.bias2) o += *reinterpret_cast<const f32x4*>(a.bias2 + (size_t)s_b2[row] * a.N + n);
+            if (a.res) o += *reinterpret_cast<const f32x4*>(a.res + pix * a.res_cs + a.res_co + n);
+            if (a.relu) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = fmaxf(o[e], 0.f);
+            }
+            *reinterpret_cast<f32x4*>(a.out + pix * a.out_cs + a.out_co + n) = o;
+          }
+        }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -611,6 +657,10 @@ int prepare(const krrn_conv_desc& d, int& tile, ConvArgs& a, int& splits, bool x
     if (splits > 1) a.ws = d.workspace;
   }
   if (splits < 1) splits = 1;
+  a.vec = !d.out_nchw && !(d.n_store & 3) && !(d.out_cs & 3) && !(d.out_co & 3) && krrn_aligned16(d.out) &&
+          (!d.scale || krrn_aligned16(d.scale)) && (!d.bias || krrn_aligned16(d.bias)) &&
+          (!d.bias2 || (!(N & 3) && krrn_aligned16(d.bias2))) &&
+          (!d.res || (!(d.res_cs & 3) && !(d.res_co & 3) && krrn_aligned16(d.res)));
   return KRRN_OK;
 }
 
