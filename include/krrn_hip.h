@@ -193,6 +193,18 @@ int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, i
 int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* U3,
                              int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                              int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
+/* A head's last 3x3 conv fused with its final 1x1 conv (nml_final, krrn.py:80-84 / 98, when it has
+ * at most 4 output channels): h = act(scale[n] * conv3x3 + bias[n] (+ res)) as
+ * krrn_conv3x3_wino_x3_f32 with n_store = N, then out[b][o][y][x] = sum_n w1[o][n] h[n] + b1[o]
+ * for o < p1 (NCHW, out_c channels per image). The N-channel map h is never written: each
+ * 64-channel block of the Winograd grid writes its 4 partial dot products per pixel to part
+ * (ceil(N / 64) * B * H * W * 4 floats, 16-byte aligned), and a second launch adds them in block
+ * order plus b1 (deterministic). w1 [4][N] f32 (rows >= p1 zero), 16-byte aligned; N % 4 == 0,
+ * 1 <= p1 <= 4; b1 may be NULL. */
+int krrn_conv3x3_wino_x3_head_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
+                                  const void* U3, int N, const float* scale, const float* bias, const float* res,
+                                  int res_cs, int res_co, int relu, const float* w1, const float* b1, int p1,
+                                  float* part, float* out, int out_c, void* stream);
 
 /* Direct conv for narrow layers: 3x3 / pad 1 / stride 1 or 2, or 1x1 / stride 1 (the HRNet
  * branches' BasicBlock convs, lib/network/hrnet/myhrnet.py:34-63, and the fuse layers' stride-2

@@ -72,6 +72,11 @@ struct WinoArgs {
   int relu;
   int vec;        // float4 epilogue (16-B aligned channel runs, n_store % 4 == 0)
   int Ht, Wt, T;  // tiles per column / row, total tiles
+  // head form (krrn_conv3x3_wino_x3_head_f32): the conv's activated output is not stored; its dot
+  // with the 4 rows of w1 ([4][N], the following 1x1 conv's weights) over this block's channels goes
+  // to part[nb][pixel][4], summed over the n-blocks by wino_head_finish_kernel
+  const float* w1;
+  float* part;
 };
 
 // Output transform Y = A^T M A + epilogue. Wave w holds row u = w of the 4x4 component grid
@@ -181,6 +186,91 @@ __device__ __forceinline__ void wino_epi_finish2d(const WinoArgs& a, const float
       }
     }
   }
+}
+
+// sum over the 16 lanes of a DPP row (every lane gets the sum): quad swaps, then half-row and row
+// mirrors
+__device__ __forceinline__ float row16_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));  // quad [1 0 3 2]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));  // quad [2 3 0 1]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));  // row_mirror
+  return x;
+}
+
+// Head epilogue: the conv's activated 2x2 pixels x 4 channels per (tile, n4) pair dotted with the
+// following 1x1 conv's 4 weight rows, summed over the 16 lanes (n4 = lane % 16) that hold the
+// tile's 64 channels, one float4 per pixel to part[nb] (the n-blocks' partials are added in order
+// by wino_head_finish_kernel: deterministic). The 128-channel map itself is never written.
+template <int WT = kWT, int GX = kGX>
+__device__ __forceinline__ void wino_epi_head2d(const WinoArgs& a, const float* smem, int b, int ty0, int tx0,
+                                                int n0, int nb) {
+  constexpr int kNP = WT * kN4 / 256;
+  static_assert(kN4 == 16, "one tile's channels = one DPP row");
+  const int tid = threadIdx.x;
+  const long long M = (long long)a.B * a.H * a.W;
+#pragma unroll
+  for (int i = 0; i < kNP; ++i) {
+    const int pr = tid + 256 * i;
+    const int n4 = pr % kN4, tl = pr / kN4;
+    const int n = n0 + 4 * n4;
+    const int ty = ty0 + tl / GX, tx = tx0 + tl % GX;
+    const bool tok = ty < a.Ht && tx < a.Wt;  // uniform over the row
+    const bool nok = n < a.n_store;
+    f32x4 c[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) c[u][q] = *reinterpret_cast<const f32x4*>(smem + ((u * 2 + q) * WT + tl) * kSP + 4 * n4);
+    f32x4 y[4];
+    y[0] = c[0][0] + c[1][0] + c[2][0];
+    y[1] = c[0][1] + c[1][1] + c[2][1];
+    y[2] = c[1][0] - c[2][0] - c[3][0];
+    y[3] = c[1][1] - c[2][1] - c[3][1];
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 scl = (nok && a.scale) ? *reinterpret_cast<const f32x4*>(a.scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 bia = (nok && a.bias) ? *reinterpret_cast<const f32x4*>(a.bias + n) : zero;
+    f32x4 w[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) w[o] = nok ? *reinterpret_cast<const f32x4*>(a.w1 + (size_t)o * a.N + n) : zero;
+    float s[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+      const bool ok = tok && nok && oy < a.H && ox < a.W;
+      f32x4 v = y[q] * scl + bia;
+      if (a.res && ok) v += *reinterpret_cast<const f32x4*>(a.res + (((size_t)b * a.H + oy) * a.W + ox) * a.res_cs + a.res_co + n);
+      if (a.relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (!ok) v = zero;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) s[q][o] = row16_sum(v[0] * w[o][0] + v[1] * w[o][1] + v[2] * w[o][2] + v[3] * w[o][3]);
+    }
+    if (n4 != 0 || !tok) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+      if (oy >= a.H || ox >= a.W) continue;
+      const size_t pix = ((size_t)b * a.H + oy) * a.W + ox;
+      *reinterpret_cast<f32x4*>(a.part + ((size_t)nb * M + pix) * 4) = f32x4{s[q][0], s[q][1], s[q][2], s[q][3]};
+    }
+  }
+}
+
+// out[b][o][p] = sum over n-blocks (in order) of part[nb][b * HW + p][o] + b1[o], o < p1
+__global__ __launch_bounds__(256) void wino_head_finish_kernel(const float* __restrict__ part, int nbn, long long M,
+                                                               int HW, const float* __restrict__ b1, int p1,
+                                                               float* __restrict__ out, int out_c) {
+  const long long m = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  f32x4 v = *reinterpret_cast<const f32x4*>(part + m * 4);
+  for (int nb = 1; nb < nbn; ++nb) v += *reinterpret_cast<const f32x4*>(part + ((size_t)nb * M + m) * 4);
+  const long long b = m / HW, p = m - b * HW;
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+    if (o < p1) out[(b * out_c + o) * HW + p] = v[o] + (b1 ? b1[o] : 0.f);
 }
 
 __global__ __launch_bounds__(256, 2) void wino_f23_ring_kernel(const WinoArgs a) {
@@ -395,6 +485,7 @@ __device__ __forceinline__ bf16x8 sub4(const u32x6& c, int o) {
   return __builtin_bit_cast(bf16x8, u32x4{c[o], c[o + 1], c[o + 2], c[o + 3]});
 }
 
+template <bool HEAD>
 __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[4 * 2 * kWT * kSP];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -566,7 +657,10 @@ __global__ __launch_bounds__(256, 2) void wino_f23_x3_kernel(const WinoArgs a) {
 #endif
   wino_epi_put(smem, acc);
   __syncthreads();
-  wino_epi_finish2d(a, smem, b, ty0, tx0, n0);
+  if constexpr (HEAD)
+    wino_epi_head2d(a, smem, b, ty0, tx0, n0, nb);
+  else
+    wino_epi_finish2d(a, smem, b, ty0, tx0, n0);
 }
 
 }  // namespace
@@ -586,6 +680,7 @@ KRRN_API int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B,
   a.U = U; a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
   a.res = res; a.res_cs = res_cs; a.res_co = res_co;
   a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.relu = relu;
+  a.w1 = nullptr; a.part = nullptr;
   a.Ht = (H + 1) / 2; a.Wt = (W + 1) / 2;
   const bool ov = !(out_cs & 3) && !(out_co & 3) && krrn_aligned16(out);
   const bool rv = !res || (!(res_cs & 3) && !(res_co & 3) && krrn_aligned16(res));
@@ -620,6 +715,7 @@ KRRN_API int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int
   a.U = reinterpret_cast<const float*>(U3); a.N = N; a.n_store = n_store; a.scale = scale; a.bias = bias;
   a.res = res; a.res_cs = res_cs; a.res_co = res_co;
   a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.relu = relu;
+  a.w1 = nullptr; a.part = nullptr;
   a.Ht = (H + 1) / 2; a.Wt = (W + 1) / 2;
   const bool ov = !(out_cs & 3) && !(out_co & 3) && krrn_aligned16(out);
   const bool rv = !res || (!(res_cs & 3) && !(res_co & 3) && krrn_aligned16(res));
@@ -633,6 +729,44 @@ KRRN_API int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int
   if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kWN);
   if (rb > 0x7fffffffLL) return KRRN_ESHAPE;
-  hipLaunchKernelGGL(wino_f23_x3_kernel, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(wino_f23_x3_kernel<false>, dim3((unsigned)rb), dim3(256), 0, (hipStream_t)stream, a);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_conv3x3_wino_x3_head_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
+                                           const void* U3, int N, const float* scale, const float* bias,
+                                           const float* res, int res_cs, int res_co, int relu, const float* w1,
+                                           const float* b1, int p1, float* part, float* out, int out_c,
+                                           void* stream) {
+  if (!in || !U3 || !w1 || !part || !out) return KRRN_EARG;
+  if (B < 1 || H < 1 || W < 1 || N < 4 || (N & 3) || p1 < 1 || p1 > 4 || out_c < p1) return KRRN_ESHAPE;
+  if (cin < 4 || (cin & 3) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(U3) || (((uintptr_t)in) & 3u) || !krrn_aligned16(w1) || !krrn_aligned16(part)) return KRRN_EALIGN;
+  if ((scale && !krrn_aligned16(scale)) || (bias && !krrn_aligned16(bias))) return KRRN_EALIGN;
+  if (res && ((res_cs & 3) || (res_co & 3) || !krrn_aligned16(res))) return KRRN_EALIGN;
+  WinoArgs a;
+  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = H; a.W = W; a.cin = cin;
+  a.img = (long long)H * W * in_cs;
+  a.U = reinterpret_cast<const float*>(U3); a.N = N; a.n_store = N; a.scale = scale; a.bias = bias;
+  a.res = res; a.res_cs = res_cs; a.res_co = res_co;
+  a.out = nullptr; a.out_cs = 0; a.out_co = 0; a.relu = relu; a.vec = 1;
+  a.w1 = w1; a.part = part;
+  a.Ht = (H + 1) / 2; a.Wt = (W + 1) / 2;
+  const long long T = (long long)B * a.Ht * a.Wt;
+  if (T > 0x7fffffffLL) return KRRN_ESHAPE;
+  a.T = (int)T;
+  const long long nrec = (long long)krrn_cdiv(cin, kWC) * 16 * N * 2;
+  if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
+  const int nbn = krrn_cdiv(N, kWN);
+  const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * nbn;
+  const long long M = (long long)B * H * W;
+  const long long fb = (M + 255) / 256;
+  if (rb > 0x7fffffffLL || fb > 0x7fffffffLL) return KRRN_ESHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wino_f23_x3_kernel<true>, dim3((unsigned)rb), dim3(256), 0, s, a);
+  const int st = krrn_launch_status();
+  if (st != KRRN_OK) return st;
+  hipLaunchKernelGGL(wino_head_finish_kernel, dim3((unsigned)fb), dim3(256), 0, s, part, nbn, M, H * W,
+                     b1, p1, out, out_c);
   return krrn_launch_status();
 }

@@ -38,6 +38,10 @@ SMALL_CONV = knobs.flag("KRRN_SMALL_CONV")
 GEMM_1X1 = knobs.flag("KRRN_GEMM_1X1")
 FUSE_ID_FIRST = knobs.flag("KRRN_FUSE_ID_FIRST")
 WINO_X3 = knobs.flag("KRRN_WINO_X3")
+# a head's final 1x1 conv with <= 4 outputs (nml_final of a one-class model) fused into the split
+# Winograd of the conv before it (krrn_conv3x3_wino_x3_head_f32): its 128-channel input map is never
+# written or re-read
+HEAD_FUSE = knobs.flag("KRRN_HEAD_FUSE")
 CONV_X3 = knobs.flag("KRRN_CONV_X3")
 # tile of the grouped transposed convs, and their k order: channel chunks of this many channels
 # outer, taps inner (krrn_conv_desc.k_chunk; 0 = tap-major)
@@ -233,14 +237,48 @@ class _Builder:
             self.emit_conv(x, spec, out, res, relu)
         return out
 
-    def conv_up2(self, x: Act, conv: nn.Module, bn: Optional[nn.Module], relu: bool = False) -> Act:
-        """conv(UpsamplingBilinear2d(scale 2)(x)) (krrn.py:56-58, 78-80): the upsample materialised
-        (resize) and the conv. Blending the upsample into the split Winograd's input staging instead
-        was measured slower and removed."""
-        H, W = 2 * x.H, 2 * x.W
-        up = self.act(H, W, x.c)
+    def conv_head(self, x: Act, conv: nn.Module, bn: Optional[nn.Module], final: nn.Conv2d, out: torch.Tensor,
+                  n_store: int) -> bool:
+        """relu(bn(conv(x))) -> final (1x1 + bias) into the NCHW map `out` (channels < n_store) as
+        one split-Winograd launch plus a partial-sum pass (krrn_conv3x3_wino_x3_head_f32), for a final
+        conv with at most 4 outputs (nml_final with one class, krrn.py:80-84, 98). False (nothing
+        emitted) when it does not apply."""
+        if not (HEAD_FUSE and WINO_X3 and isinstance(conv, nn.Conv2d) and tuple(final.kernel_size) == (1, 1)
+                and tuple(final.stride) == (1, 1) and final.in_channels == conv.out_channels
+                and n_store <= min(4, final.out_channels) and x.cs % 2 == 0 and x.co % 2 == 0):
+            return False
+        spec = ops.make_conv(conv, bn, self.dev, cin_p=x.cp)
+        Ho, Wo = ops.conv_out_hw(spec, x.H, x.W)
+        M = x.B * Ho * Wo
+        if not ops.wino_eligible(spec, M) or (Ho, Wo) != (x.H, x.W):
+            return False
+        np_ = pad4(spec.cout)
+        U = ops.wino_weights_x3(ops.wino_weights(conv, self.dev, cin_p=x.cp))
+        w1 = torch.zeros(4, np_, device=self.dev)
+        w1[:final.out_channels, :spec.cout] = final.weight.detach().reshape(final.out_channels, -1).float().to(self.dev)
+        b1 = None
+        if final.bias is not None:
+            b1 = torch.zeros(4, device=self.dev)
+            b1[:final.out_channels] = final.bias.detach().float().to(self.dev)
+        self.specs += [spec, U, w1] + ([b1] if b1 is not None else [])
+        part = self.plan.scratch(((np_ + 63) // 64) * M * 4)
+        tiles = x.B * ((Ho + 1) // 2) * ((Wo + 1) // 2)
+        pipe = 2.0 * 16 * spec.cin_p * np_ * tiles
+        meta = dict(kernel="wino_f23_x3_head", tag="conv_wino_head", M=M, N=np_, K=spec.cin_p * 9,
+                    flops=2.0 * spec.cin * spec.cout * 9 * M + 2.0 * spec.cout * n_store * M,
+                    mfma_flops=pipe * 6 / 16, mfma_bf16_flops=pipe * 6)
+        self.plan.add("krrn_conv3x3_wino_x3_head_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(U), np_,
+                      ptr(spec.scale), ptr(spec.bias), ptr(None), 0, 0, 1, ptr(w1), ptr(b1), n_store, ptr(part),
+                      ptr(out), out.shape[1], meta=meta)
+        return True
+
+    def upsample2(self, x: Act) -> Act:
+        """UpsamplingBilinear2d(scale 2)(x) (krrn.py:56, 78; align_corners=True) materialised for the
+        conv after it. Blending the upsample into the split Winograd's input staging instead was
+        measured slower and removed."""
+        up = self.act(2 * x.H, 2 * x.W, x.c)
         self.resize(x, up, align=True)
-        return self.conv(up, conv, bn, relu=relu)
+        return up
 
     def emit_gemm(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool) -> bool:
         """A wide 1x1 / stride-1 conv (layer1's Bottleneck projections, myhrnet.py:66-103) is a plain

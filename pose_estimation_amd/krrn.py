@@ -203,14 +203,17 @@ class KRRNPlan:
 
     def _head_tail(self, bld: _Builder, x: Act, convs, final: nn.Conv2d, out: torch.Tensor, n_store: int):
         """A head's full-resolution tail (krrn.py:56-65 / 78-84): UpsamplingBilinear2d(x2) ->
-        [conv3x3 + BN + ReLU] x len(convs) -> the final 1x1 (+ bias) into the NCHW map `out`, the
-        upsample folded as the first conv's input (conv_up2). Running it in crop chunks through
-        reused chunk buffers (the upsampled map kept in the Infinity Cache) measured 0.8 % slower
-        (DESIGN.md section 4, round 5)."""
+        [conv3x3 + BN + ReLU] x len(convs) -> the final 1x1 (+ bias) into the NCHW map `out`; a
+        final with at most 4 outputs runs inside the last conv's launch (_Builder.conv_head).
+        Running the tail in crop chunks through reused chunk buffers (the upsampled map kept in the
+        Infinity Cache) measured 0.8 % slower."""
         spec = ops.make_conv(final, None, self.plan.device, cin_p=pad4(convs[-1][0].out_channels))
         bld.specs.append(spec)
-        h = bld.conv_up2(x, convs[0][0], convs[0][1], relu=True)
-        for conv, bn in convs[1:]:
+        h = bld.upsample2(x)
+        for i, (conv, bn) in enumerate(convs):
+            # the last conv and the final 1x1 as one launch where the final is narrow (bld.conv_head)
+            if i == len(convs) - 1 and bld.conv_head(h, conv, bn, final, out, n_store):
+                return
             h = bld.conv(h, conv, bn, relu=True)
         self._nchw_conv(h, spec, out, n_store)
 

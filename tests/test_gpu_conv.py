@@ -309,6 +309,49 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     torch.testing.assert_close(got3, got, rtol=1e-5, atol=2e-6 * scale)
 
 
+@pytest.mark.parametrize("cin,cout,H,W,co,p1,with_res", [
+    (128, 128, 120, 120, 0, 3, False), (64, 72, 17, 23, 4, 4, True), (20, 132, 9, 8, 0, 1, True),
+    (36, 40, 7, 9, 8, 2, False)])
+def test_conv3x3_winograd_head(dev, cin, cout, H, W, co, p1, with_res):
+    """krrn_conv3x3_wino_x3_head_f32: the last head conv (+ BN, residual, ReLU) and a <= 4-output
+    1x1 + bias in one launch (NML's 120-px conv + nml_final at B = 3, ragged 64-channel blocks, odd
+    maps) vs torch fp32; the NCHW channels past p1 are not written."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, ptr
+    g = torch.Generator().manual_seed(cin + 3 * cout + H + p1)
+    B = 3
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+    final = nn.Conv2d(cout, p1, 1)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+        final.weight.copy_(0.1 * torch.randn(final.weight.shape, generator=g))
+        final.bias.copy_(0.1 * torch.randn(p1, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, W, generator=g)
+    res = torch.randn(B, cout, H, W, generator=g) if with_res else None
+    h = bn(conv(x))
+    ref = final(torch.relu(h + res if with_res else h)).detach()
+    xa = _nhwc(x, dev, cs=ops.pad4(cin) + co + 4, co=co)
+    spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
+    U3 = ops.wino_weights_x3(ops.wino_weights(conv, dev, cin_p=ops.pad4(cin)))
+    np_ = ops.pad4(cout)
+    w1 = torch.zeros(4, np_, device=dev)
+    w1[:p1, :cout] = final.weight.detach().reshape(p1, cout).to(dev)
+    b1 = final.bias.detach().to(dev).contiguous()
+    ra = _nhwc(res, dev) if with_res else None
+    part = torch.full((((np_ + 63) // 64) * B * H * W * 4,), float("nan"), device=dev)
+    out = torch.full((B, p1 + 1, H, W), -7.0, device=dev)
+    L = _lib.lib()
+    _lib.check(L.krrn_conv3x3_wino_x3_head_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_,
+                                               ptr(spec.scale), ptr(spec.bias), ptr(ra.t) if ra else ptr(None),
+                                               ra.cs if ra else 0, 0, 1, ptr(w1), ptr(b1), p1, ptr(part), ptr(out),
+                                               p1 + 1, P(torch.cuda.current_stream().cuda_stream)), "wino_head")
+    torch.cuda.synchronize()
+    got = out.cpu()
+    torch.testing.assert_close(got[:, :p1], ref, **TOL)
+    assert torch.all(got[:, p1] == -7.0)
+
+
 @pytest.mark.parametrize("B,cin,cout,H,W,co,nw,ks,k,st", [
     (3, 20, 18, 30, 30, 0, 2, 1, 3, 1), (64, 144, 144, 4, 4, 0, 1, 4, 3, 1), (8, 36, 36, 15, 15, 4, 3, 2, 3, 1),
     (5, 72, 72, 8, 8, 0, 1, 4, 3, 1), (2, 12, 40, 7, 9, 0, 2, 2, 3, 1), (3, 4, 8, 5, 6, 0, 1, 1, 3, 1),
