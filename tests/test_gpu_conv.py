@@ -262,6 +262,39 @@ def test_convT_group_kchunk(dev, cin, k, op, x3, q):
     torch.testing.assert_close(got[1], got[0], rtol=1e-5, atol=2e-6 * float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("x3,tile", [(False, 8), (False, 6), (True, 1), (True, 8)])
+def test_conv_epilogue_float4_and_scalar(dev, x3, tile):
+    """The implicit-GEMM conv's NHWC epilogue: float4 channel runs through the per-wave LDS square
+    when every operand is 16-B aligned (out_co = 0), the per-element form otherwise (out_co = 1,
+    res_co = 1); both with a per-crop bias2, a residual and a row tail, vs torch fp32 and each other."""
+    g = torch.Generator().manual_seed(11 + tile + 5 * x3)
+    B, cin, cout, H = 3, 36, 40, 13
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(0.05 * torch.randn(conv.weight.shape, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, H, generator=g)
+    res = torch.randn(B, cout, H, H, generator=g)
+    b2 = torch.randn(B, cout, generator=g)
+    ref = torch.relu(bn(conv(x)) + b2[:, :, None, None] + res).detach()
+    spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
+    xa = _nhwc(x, dev)
+    b2d = b2.to(dev).contiguous()
+    got = []
+    for co in (0, 1):
+        ra = _nhwc(res, dev, cs=cout + 8, co=co)
+        out = ops.new_act(B, H, H, cout, dev, cs=cout + 8)
+        out.t.fill_(7.0)
+        o = out.slice(co, cout)
+        ops.conv2d(xa, spec, o, res=ra, relu=True, bias2=b2d, b2_div=H * H, tile=tile, x3=x3)
+        torch.cuda.synchronize()
+        t = out.t.cpu()
+        got.append(t[..., co:co + cout].permute(0, 3, 1, 2))
+        torch.testing.assert_close(got[-1], ref, **TOL)
+        assert torch.all(t[..., :co] == 7.0) and torch.all(t[..., co + cout:] == 7.0)
+    torch.testing.assert_close(got[0], got[1], rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("cin,cout,H,W,co", [(128, 128, 30, 30, 0), (64, 72, 17, 23, 4), (272, 272, 15, 15, 0),
                                              (36, 40, 9, 8, 8), (20, 132, 61, 35, 0), (128, 64, 120, 120, 0)])
 def test_conv3x3_winograd(dev, cin, cout, H, W, co):
