@@ -186,7 +186,9 @@ def test_config2_full_batch(models, dev):
     d = make_batch(B, S, N, seed=31)
     perms = _draw_perms(N, 13)
     out = _check_parity(m, o, dev, B, S, N, d, crops=[0, 31, 63], perms=perms)
-    fb64 = {k: v.cpu() for k, v in m.get_plan(B, S, N, True).fusion_bufs.items() if k in _DECISIONS}
+    plan64 = m.get_plan(B, S, N, True)
+    fb64 = {k: v.cpu() for k, v in plan64.fusion_bufs.items() if k in _DECISIONS + ("PV2",)}
+    p9_64 = plan64.p9.cpu()
     two = [0, 63]
     d2 = {k: d[k][two] for k in ("img_croped", "cloud", "choose", "cls_id")}
     o2 = m(d2["img_croped"].to(dev), d2["cloud"].to(dev), d2["choose"].to(dev), d2["cls_id"].to(dev),
@@ -199,12 +201,20 @@ def test_config2_full_batch(models, dev):
     # the discrete decisions over *predicted* coordinates (x / n pool kNNs, 9-D idx2) may flip
     # between the two batch shapes (different tiles / split-K -> different f32 rounding of the
     # maps); pred_t must agree to T_ATOL when they all agree, to T_ATOL_FLIP otherwise
-    fb2 = m.get_plan(2, S, N, True).fusion_bufs
-    agree = {k: float((fb64[k][two] == fb2[k].cpu()).float().mean()) for k in _DECISIONS}
+    plan2 = m.get_plan(2, S, N, True)
+    fb2 = {k: v.cpu() for k, v in plan2.fusion_bufs.items() if k in _DECISIONS + ("PV2",)}
+    agree = {k: float((fb64[k][two] == fb2[k]).float().mean()) for k in _DECISIONS}
     e = float((out["pred_t"][two].cpu() - o2["pred_t"].cpu()).abs().max())
     print(f"  B=64 vs B=2 pred_t: {e:.2e} m, decision agreement {agree}")
     assert agree["pool_v"] == 1.0 and agree["pool2"] == 1.0
-    assert all(v > 0.99 for v in agree.values()), agree
+    # every differing decision is a near-tie of the two runs' own coordinates (tests/parity.py)
+    p9_2 = plan2.p9.cpu()
+    for k, c0, q in (("pool_x", 3, perms[1]), ("pool_n", 6, perms[2])):
+        n_bad, n_tie = _knn_flips_at_ties(fb64[k][two], fb2[k], p9_64[two][..., c0:c0 + 3], p9_2[..., c0:c0 + 3], q,
+                                          "B64/B2 " + k)
+        assert n_bad == n_tie, (k, n_bad, n_tie)
+    n_bad, n_tie = _knn_flips_at_ties(fb64["idx2"][two], fb2["idx2"], fb64["PV2"][two], fb2["PV2"], None, "B64/B2 idx2")
+    assert n_bad == n_tie, ("idx2", n_bad, n_tie)
     assert e < (T_ATOL if all(v == 1.0 for v in agree.values()) else T_ATOL_FLIP)
     for name in ("mask", "region"):
         n_bad = int((out[name][two].argmax(1) != o2[name].argmax(1)).sum())
