@@ -42,6 +42,13 @@ WINO_X3 = knobs.flag("KRRN_WINO_X3")
 # Winograd of the conv before it (krrn_conv3x3_wino_x3_head_f32): its 128-channel input map is never
 # written or re-read
 HEAD_FUSE = knobs.flag("KRRN_HEAD_FUSE")
+# the fuse-layer work that reads only branch j's output (the 1x1 convs of the j > i terms, all but
+# the last stride-2 conv of the j < i chains) runs on branch j's stream right after its blocks,
+# beside the other branches' tails, instead of after the join on the output's stream
+FUSE_EARLY = knobs.flag("KRRN_FUSE_EARLY")
+# between two modules of a stage, branch i of the next module waits only for fuse output i (the same
+# stream) instead of a join of every stream followed by a fork
+MODULE_STREAMS = knobs.flag("KRRN_MODULE_STREAMS")
 CONV_X3 = knobs.flag("KRRN_CONV_X3")
 # tile of the grouped transposed convs, and their k order: channel chunks of this many channels
 # outer, taps inner (krrn_conv_desc.k_chunk; 0 = tap-major)
@@ -441,9 +448,13 @@ class _Builder:
         res = x if blk.downsample is None else self.conv(x, blk.downsample[0], blk.downsample[1])
         return self.conv(h, blk.conv3, blk.bn3, res=res, relu=True)
 
-    def hr_module(self, xs: List[Act], m: HighResolutionModule, outs: Optional[List[Optional[Act]]] = None) -> List[Act]:
+    def hr_module(self, xs: List[Act], m: HighResolutionModule, outs: Optional[List[Optional[Act]]] = None,
+                  fork_in: bool = True, join_out: bool = True) -> List[Act]:
         """myhrnet.py:226-250. Branch i (and later fuse output i) runs on plan stream i: the
-        branches are independent until the fuse, and the fuse outputs are independent again."""
+        branches are independent until the fuse, and the fuse outputs are independent again.
+        fork_in = False: xs[i] was produced on stream i (the previous module's fuse output i), so
+        branch i needs no fork from stream 0; join_out = False: the outputs stay on their streams for
+        the next module (the caller joins after the last one)."""
         plan = self.plan
         nb = m.num_branches
         side = list(range(1, nb))
@@ -451,14 +462,18 @@ class _Builder:
             len(m.branches[i]) == len(m.branches[0]) for i in range(nb)) and all(
             isinstance(b, BasicBlock) and b.downsample is None for br in m.branches for b in br)
         ys = self.branches_grouped(xs, m) if groupable else None
+        pre = {}
         if ys is None:
             ys = []
-            plan.fork(side)
+            if fork_in:
+                plan.fork(side)
             for i, x in enumerate(xs):
                 with plan.on_stream(i):
                     y = x
                     for blk in m.branches[i]:
                         y = self.basic(y, blk)
+                    if nb > 1 and FUSE_EARLY:
+                        pre.update(self._fuse_terms_from(y, m, i))
                 ys.append(y)
             plan.join(side)
         if nb == 1:
@@ -467,11 +482,31 @@ class _Builder:
         plan.fork(side)
         for i in range(nb):
             with plan.on_stream(i):
-                fused.append(self._fuse_output(ys, m, i, outs[i] if outs is not None else None))
-        plan.join(side)
+                fused.append(self._fuse_output(ys, m, i, outs[i] if outs is not None else None, pre))
+        if join_out:
+            plan.join(side)
         return fused
 
-    def _fuse_output(self, ys: List[Act], m: HighResolutionModule, i: int, out: Optional[Act]) -> Act:
+    def _fuse_terms_from(self, y: Act, m: HighResolutionModule, j: int) -> dict:
+        """The fuse-layer work that reads only branch j's output y (myhrnet.py:177-225), keyed by
+        (output i, j): for i < j the 1x1 conv + BN at branch j's resolution (upsampled and added by
+        _fuse_output), for i > j the stride-2 chain but its last conv (which adds into output i).
+        Emitted on branch j's stream right after its blocks: the same launches as _fuse_output's own
+        (bit-identical results), started before the other branches have finished."""
+        terms = {}
+        for i in range(m.num_branches):
+            if i < j:
+                seq = m.fuse_layers[i][j]
+                terms[(i, j)] = self.conv(y, seq[0], seq[1])
+            elif i > j:
+                h = y
+                for sub in m.fuse_layers[i][j][:-1]:
+                    h = self.conv(h, sub[0], sub[1], relu=True)
+                terms[(i, j)] = h
+        return terms
+
+    def _fuse_output(self, ys: List[Act], m: HighResolutionModule, i: int, out: Optional[Act],
+                     pre: Optional[dict] = None) -> Act:
         """relu(sum_j fuse_layers[i][j](ys[j])) (myhrnet.py:232-248). With FUSE_ID_FIRST the identity
         term opens the sum (read in place) and every other term adds it in its producer's epilogue
         (conv residual / resize add), so no separate add launch exists; the f32 summation order then
@@ -490,13 +525,14 @@ class _Builder:
                     acc = out
             elif j > i:
                 seq = m.fuse_layers[i][j]
-                low = self.conv(ys[j], seq[0], seq[1])
+                low = pre[(i, j)] if pre and (i, j) in pre else self.conv(ys[j], seq[0], seq[1])
                 self.resize(low, out, add=acc, align=False, relu=last)
                 acc = out
             else:
                 chain = m.fuse_layers[i][j]
-                h = ys[j]
-                for k, sub in enumerate(chain):
+                h, first = (pre[(i, j)], len(chain) - 1) if pre and (i, j) in pre else (ys[j], 0)
+                for k in range(first, len(chain)):
+                    sub = chain[k]
                     if k == len(chain) - 1:
                         h = self.conv(h, sub[0], sub[1], out=out, res=acc, relu=last)
                     else:
@@ -538,7 +574,8 @@ def build_hrnet_plan(net: HRNet, plan: Plan, x: Act) -> Tuple[Act, Act, list]:
                     src = bld.conv(src, sub[0], sub[1], relu=True)
                 xl.append(src)
         for mi, m in enumerate(stage):
-            xl = bld.hr_module(xl, m)
+            chain = MODULE_STREAMS and m.num_branches > 1 and not HR_GROUP  # the grouped form runs on stream 0
+            xl = bld.hr_module(xl, m, fork_in=not chain or mi == 0, join_out=not chain or mi == len(stage) - 1)
         ylist = xl
     # upsample + concat (myhrnet.py:511-516) straight into channel slices
     H0, W0 = ylist[0].H, ylist[0].W
