@@ -49,6 +49,9 @@ FUSE_EARLY = knobs.flag("KRRN_FUSE_EARLY")
 # between two modules of a stage, branch i of the next module waits only for fuse output i (the same
 # stream) instead of a join of every stream followed by a fork
 MODULE_STREAMS = knobs.flag("KRRN_MODULE_STREAMS")
+# ... and across stage boundaries: a stage's last module keeps its outputs on their streams, and the
+# next stage's transition conv for branch i runs on stream i after a wait on its source's stream
+STAGE_STREAMS = knobs.flag("KRRN_STAGE_STREAMS")
 CONV_X3 = knobs.flag("KRRN_CONV_X3")
 # tile of the grouped transposed convs, and their k order: channel chunks of this many channels
 # outer, taps inner (krrn_conv_desc.k_chunk; 0 = tap-major)
@@ -550,32 +553,47 @@ def build_hrnet_plan(net: HRNet, plan: Plan, x: Act) -> Tuple[Act, Act, list]:
         h = bld.bottleneck(h, blk)
     ylist = [h]
     nstages = len(net.spec.stages)
+    on_streams = False  # ylist[k] lives on plan stream k (the previous stage was not joined)
     for si in range(nstages):
         trans = getattr(net, f"transition{si + 1}")
         stage = getattr(net, f"stage{si + 2}")
         nb = net.stage_branches[si]
+        # per-stream stages: every module of the stage chains per stream (the grouped form runs on
+        # stream 0, so not with it)
+        cross = STAGE_STREAMS and MODULE_STREAMS and not HR_GROUP and all(m.num_branches > 1 for m in stage)
         xl = []
         for i in range(nb):
             t = trans[i]
             if t is None:
-                xl.append(ylist[i])
+                if cross and not on_streams:
+                    plan.sync(0, i)  # the previous stage was joined into stream 0
+                xl.append(ylist[i])  # on stream i (on_streams) or joined into stream 0
             else:
                 # myhrnet.py:482-507: transition1 reads the stem output; transition2 reads
                 # y_list[-1] for every non-None entry; transition3 reads y_list[i] for
                 # i < NUM_BRANCHES(stage3) and y_list[-1] otherwise.
                 if si == 0:
-                    src = ylist[0]
+                    k = 0
                 elif si == 1:
-                    src = ylist[-1]
+                    k = len(ylist) - 1
                 else:
-                    src = ylist[i] if i < len(ylist) else ylist[-1]
+                    k = i if i < len(ylist) else len(ylist) - 1
+                src = ylist[k]
                 chain = [t] if isinstance(t[0], nn.Conv2d) else list(t)
-                for sub in chain:
-                    src = bld.conv(src, sub[0], sub[1], relu=True)
+                sid = i if cross else 0
+                if cross:
+                    plan.sync(k if on_streams else 0, i)
+                with plan.on_stream(sid):
+                    for sub in chain:
+                        src = bld.conv(src, sub[0], sub[1], relu=True)
                 xl.append(src)
+        last_stage = si == nstages - 1
         for mi, m in enumerate(stage):
             chain = MODULE_STREAMS and m.num_branches > 1 and not HR_GROUP  # the grouped form runs on stream 0
-            xl = bld.hr_module(xl, m, fork_in=not chain or mi == 0, join_out=not chain or mi == len(stage) - 1)
+            fork_in = not chain or (mi == 0 and not cross)
+            join_out = not chain or (mi == len(stage) - 1 and (last_stage or not cross))
+            xl = bld.hr_module(xl, m, fork_in=fork_in, join_out=join_out)
+        on_streams = cross and not last_stage
         ylist = xl
     # upsample + concat (myhrnet.py:511-516) straight into channel slices
     H0, W0 = ylist[0].H, ylist[0].W

@@ -225,6 +225,12 @@ class Plan:
             if s != 0:
                 self.ops.append(Sync(s, 0))
 
+    def sync(self, src: int, dst: int):
+        """Stream `dst` waits for all work so far on stream `src`."""
+        if src != dst:
+            self.nstreams = max(self.nstreams, src + 1, dst + 1)
+            self.ops.append(Sync(src, dst))
+
     def side_streams(self) -> List[torch.cuda.Stream]:
         while len(self._side) < self.nstreams - 1:
             self._side.append(torch.cuda.Stream(self.device))
