@@ -111,8 +111,82 @@ def _bn1d(bn: nn.BatchNorm1d, device):
     return s.float().to(device), b.float().to(device)
 
 
+class _Emit:
+    """The fusion's launch helpers (kNN, gather-conv, GEMM) bound to one plan and batch."""
+
+    def __init__(self, fu: FusionNetLite, plan: Plan, B: int, keep: list):
+        self.plan, self.B, self.dev, self.S, self.keep = plan, B, plan.device, fu.support_num, keep
+
+    def knn(self, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, out):
+        self.plan.add("krrn_knn_f32", q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, self.B, ptr(out))
+
+    def gcn(self, idx, n, k, v, v_bs, d, dn, C, Y, bn, relu, out, o_bs, o_st, Bc=None, v_st=9):
+        self.keep.append(dn)
+        s, b = (None, None) if bn is None else bn
+        self.keep.extend([s, b])
+        self.plan.add("krrn_gcn_conv_f32", ptr(idx), n, k, v, v_bs, v_st, d, ptr(dn), self.S, C, ptr(Y), ptr(s), ptr(b),
+                      int(relu), out, o_bs, o_st, self.B if Bc is None else Bc)
+
+    def gemm(self, a, a_cs, a_co, M, layer: "Conv_layer", out):
+        spec = ops.make_linear(layer.weights.detach().t(), layer.bias, None, self.dev,
+                               cin_p=ops.pad4(layer.in_channel))
+        self.keep.append(spec)
+        np_ = ops.pad4(spec.cout)
+        if add_gemm(self.plan, a=a, a_off=a_co, lda=a_cs, M=M, wt=spec.wt[0], K=spec.cin_p, N=np_, scale=spec.scale,
+                    bias=spec.bias, out=out, ldo=out.shape[-1], relu=False, cin=spec.cin, cout=spec.cout,
+                    tag="gcn_gemm"):
+            return
+        add_conv(self.plan, x=ptr(a), x_cs=a_cs, x_co=a_co, B=1, Hi=1, Wi=M, cin_p=spec.cin_p, Hg=1, Wg=M, in_s=1,
+                 taps=[(0, 0)], wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
+                 out=ptr(out), out_cs=out.shape[-1], out_co=0, Ho=1, Wo=M, cin=spec.cin, cout=spec.cout,
+                 tag="gcn_gemm")
+
+
+def _off(t, floats):
+    return ptr(t) if floats == 0 else type(ptr(t))(t.data_ptr() + 4 * floats)
+
+
+def _level0_branch(e: _Emit, fu: FusionNetLite, bi: int, br: str, N: int, idx0, v, v_bs, v_st, F0, Y1b, feat1, cy: int):
+    """Level-0 branch `br` up to its pool (fusion.py:183-196): conv_0 (Conv_surface + ReLU) and
+    conv_1 (Conv_layer + BN1d + ReLU, its GEMM and gather-conv in crop chunks of cy) on the
+    branch's vertices v (rows of stride v_st floats)."""
+    B = e.B
+    c0 = getattr(fu, f"conv_0_{br}")
+    e.gcn(idx0, N, fu.neighbor_num, v, v_bs, 3, _dn(c0.directions, e.dev), 128, None, None, True,
+          _off(F0, 128 * bi), N * 384, 384, v_st=v_st)
+    c1 = getattr(fu, f"conv_1_{br}")
+    dn1, bn1 = _dn(c1.directions, e.dev), _bn1d(getattr(fu, f"bn1_{br}"), e.dev)
+    for b0 in range(0, B, cy):
+        nb = min(cy, B - b0)
+        e.gemm(F0[b0:b0 + nb], 384, 128 * bi, nb * N, c1, Y1b)
+        vb = type(v)(v.value + 4 * b0 * v_bs)
+        e.gcn(idx0[b0:b0 + nb], N, fu.neighbor_num, vb, v_bs, 3, dn1, 128, Y1b, bn1, True,
+              _off(feat1[b0:], 128 * bi), N * 384, 384, Bc=nb, v_st=v_st)
+
+
+def emit_fusion_cloud_part(fu: FusionNetLite, plan: Plan, B: int, N: int, cloud: torch.Tensor) -> dict:
+    """The fusion work that reads only the input cloud ([B, N, 3]): the level-0 kNN idx0
+    (fusion.py:175) and the v branch's conv_0 / conv_1 (fusion.py:183-189, whose vertices are the
+    cloud). KRRNPlan emits it at the start of the forward on a side stream, beside the HRNet
+    phase that leaves most of the chip idle; build_fusion_plan(early=...) then skips it. Same
+    launches on the same values (the cloud is p9's first three channels): bit-identical."""
+    k0 = fu.neighbor_num
+    keep: list = []
+    e = _Emit(fu, plan, B, keep)
+    cy = B if not FUSION_CHUNK or FUSION_CHUNK >= B else FUSION_CHUNK
+    idx0 = plan.buf((B, N, k0), torch.int32)
+    F0 = plan.buf((B, N, 384))
+    feat1 = plan.buf((B, N, 384))
+    Y1v = plan.buf((cy * N, (fu.support_num + 1) * 128))
+    e.knn(ptr(cloud), N * 3, 3, N, ptr(None), ptr(cloud), N * 3, 3, N, 3, k0, 1, 0, idx0)
+    _level0_branch(e, fu, 0, "v", N, idx0, ptr(cloud), N * 3, 3, F0, Y1v, feat1, cy)
+    plan.buffers.append(keep)
+    return dict(idx0=idx0, F0=F0, feat1=feat1, Y1v=Y1v)
+
+
 def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.Tensor, perms: Dict[str, torch.Tensor],
-                      hooks: Optional[Dict[str, List[Callable[[dict], None]]]] = None, materialize: bool = True):
+                      hooks: Optional[Dict[str, List[Callable[[dict], None]]]] = None, materialize: bool = True,
+                      early: Optional[dict] = None):
     """Emit FusionNetLite.forward for P9 = [cloud | xyz_emb | nml_emb] ([B, N, 9] f32).
 
     perms: int32 device buffers 'v', 'x', 'n' ([N1] each, permutations of N), 'p1' ([N1]),
@@ -122,6 +196,7 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     point (feat1, feat2), e.g. to fork independent work onto a side stream where the fusion
     leaves the chip underused. materialize=False skips writing the 1280-wide concat (returns None
     for it): its only consumer, TBase conv1, reads the level rows by linearity.
+    early: emit_fusion_cloud_part's buffers when that part was emitted already (joined before this).
     """
     hooks = hooks or {}
     dev = plan.device
@@ -132,16 +207,16 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
         raise ValueError(f"num_points={N} too small for the 3-level GCN (needs N/16 >= 8)")
     keep = []
     i32 = torch.int32
-    idx0 = plan.buf((B, N, k0), i32)
-    F0 = plan.buf((B, N, 384))
+    idx0 = early["idx0"] if early else plan.buf((B, N, k0), i32)
+    F0 = early["F0"] if early else plan.buf((B, N, 384))
     # one GEMM-output buffer per branch: the three branches run on their own plan streams. With
     # FUSION_CHUNK = c the level-0 GEMM and its gather-conv run in crop chunks of c through a
     # c-crop buffer per branch (crops are independent: a point's neighbours are in its own crop),
     # so Y is written and re-read while it sits in the Infinity Cache instead of one 262 MB HBM
     # round trip per branch; the buffer is reused by every chunk
     cy = B if not FUSION_CHUNK or FUSION_CHUNK >= B else FUSION_CHUNK
-    Y1 = [plan.buf((cy * N, (S + 1) * 128)) for _ in range(3)]
-    feat1 = plan.buf((B, N, 384))
+    Y1 = [early["Y1v"] if early and i == 0 else plan.buf((cy * N, (S + 1) * 128)) for i in range(3)]
+    feat1 = early["feat1"] if early else plan.buf((B, N, 384))
     nb4 = {br: plan.buf((B, N1, 4), i32) for br in ("v", "x", "n")}
     V1 = plan.buf((B, N1, 9))
     FP1 = plan.buf((B, N1, 384))
@@ -161,50 +236,19 @@ def build_fusion_plan(fu: FusionNetLite, plan: Plan, B: int, N: int, p9: torch.T
     nn2 = plan.buf((B, N), i32)
     feat = plan.buf((B, N, 1280)) if materialize else None
 
-    def knn(q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, out):
-        plan.add("krrn_knn_f32", q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, B, ptr(out))
-
-    def gcn(idx, n, k, v, v_bs, d, dn, C, Y, bn, relu, out, o_bs, o_st, Bc=None):
-        keep.append(dn)
-        s, b = (None, None) if bn is None else bn
-        keep.extend([s, b])
-        plan.add("krrn_gcn_conv_f32", ptr(idx), n, k, v, v_bs, 9, d, ptr(dn), S, C, ptr(Y), ptr(s), ptr(b), int(relu),
-                 out, o_bs, o_st, B if Bc is None else Bc)
-
-    def gemm(a, a_cs, a_co, M, layer: Conv_layer, out):
-        spec = ops.make_linear(layer.weights.detach().t(), layer.bias, None, dev,
-                               cin_p=ops.pad4(layer.in_channel))
-        keep.append(spec)
-        np_ = ops.pad4(spec.cout)
-        if add_gemm(plan, a=a, a_off=a_co, lda=a_cs, M=M, wt=spec.wt[0], K=spec.cin_p, N=np_, scale=spec.scale,
-                    bias=spec.bias, out=out, ldo=out.shape[-1], relu=False, cin=spec.cin, cout=spec.cout,
-                    tag="gcn_gemm"):
-            return
-        add_conv(plan, x=ptr(a), x_cs=a_cs, x_co=a_co, B=1, Hi=1, Wi=M, cin_p=spec.cin_p, Hg=1, Wg=M, in_s=1,
-                 taps=[(0, 0)], wt=ptr(spec.wt[0]), N=np_, n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias),
-                 out=ptr(out), out_cs=out.shape[-1], out_co=0, Ho=1, Wo=M, cin=spec.cin, cout=spec.cout,
-                 tag="gcn_gemm")
-
-    def off(t, floats):
-        return ptr(t) if floats == 0 else type(ptr(t))(t.data_ptr() + 4 * floats)
+    e = _Emit(fu, plan, B, keep)
+    knn, gcn, gemm, off = e.knn, e.gcn, e.gemm, _off
 
     # level 0: idx0 = kNN(cloud, 10) (fusion.py:175)
     # level 0: idx0 = kNN(cloud, 10) (fusion.py:175); then the v / x / n branches (conv_0,
     # conv_1 + BN + ReLU, pool_1_*) are independent until the concat: branch bi on stream bi
-    knn(off(p9, 0), N * 9, 9, N, ptr(None), off(p9, 0), N * 9, 9, N, 3, k0, 1, 0, idx0)
+    if not early:
+        knn(off(p9, 0), N * 9, 9, N, ptr(None), off(p9, 0), N * 9, 9, N, 3, k0, 1, 0, idx0)
     plan.fork([1, 2])
     for bi, br in enumerate(("v", "x", "n")):
         with plan.on_stream(bi):
-            c0 = getattr(fu, f"conv_0_{br}")
-            gcn(idx0, N, k0, off(p9, 3 * bi), N * 9, 3, _dn(c0.directions, dev), 128, None, None, True,
-                off(F0, 128 * bi), N * 384, 384)
-            c1 = getattr(fu, f"conv_1_{br}")
-            dn1, bn1 = _dn(c1.directions, dev), _bn1d(getattr(fu, f"bn1_{br}"), dev)
-            for b0 in range(0, B, cy):
-                nb = min(cy, B - b0)
-                gemm(F0[b0:b0 + nb], 384, 128 * bi, nb * N, c1, Y1[bi])
-                gcn(idx0[b0:b0 + nb], N, k0, off(p9[b0:], 3 * bi), N * 9, 3, dn1, 128, Y1[bi], bn1, True,
-                    off(feat1[b0:], 128 * bi), N * 384, 384, Bc=nb)
+            if not (early and bi == 0):
+                _level0_branch(e, fu, bi, br, N, idx0, off(p9, 3 * bi), N * 9, 9, F0, Y1[bi], feat1, cy)
             # pools (fusion.py:197-202): kNN(4) at the sampled rows, max, vertex gather
             perm = perms[br]
             knn(off(p9, 3 * bi), N * 9, 9, N1, ptr(perm), off(p9, 3 * bi), N * 9, 9, N, 3, 4, 1, 0, nb4[br])

@@ -31,6 +31,7 @@ KNOBS: Dict[str, Tuple[Optional[str], str]] = {
     "KRRN_FUSE_EARLY": ("1", "HRNet fuse terms that read one branch start on that branch's stream before the join"),
     "KRRN_MODULE_STREAMS": ("1", "consecutive HRNet modules of a stage keep each branch on its stream (no barrier between them)"),
     "KRRN_STAGE_STREAMS": ("1", "with KRRN_MODULE_STREAMS, HRNet stages chain per branch stream too (transitions on their branch's stream)"),
+    "KRRN_FUSION_EARLY": ("1", "the fusion work that reads only the input cloud runs beside the HRNet phase (side stream)"),
     "KRRN_HEAD_FUSE": ("1", "a <= 4-output final 1x1 fused into the head's last split Winograd; 0 = two launches"),
     "KRRN_SMALL_CONV": ("1", "HRNet branch / fuse convs on the LDS-slab conv_small kernel; 0 = implicit GEMM"),
     "KRRN_HR_GROUP": ("0", "the four branches' j-th convs as one grouped conv_small launch (measured "

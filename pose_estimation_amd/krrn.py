@@ -37,7 +37,7 @@ import torch.nn as nn
 
 from . import knobs, ops
 from .config import CONFIG
-from .fusion import FEAT_SID, FusionNetLite, build_fusion_plan, level_sizes
+from .fusion import FEAT_SID, FusionNetLite, build_fusion_plan, emit_fusion_cloud_part, level_sizes
 from .hrnet import _Builder, build_hrnet, build_hrnet_plan
 from .ops import Act, pad4
 from .posenet import PoseNet, build_tbase_plan, emit_tbase_level1
@@ -52,6 +52,9 @@ TBASE_EARLY = knobs.flag("KRRN_TBASE_EARLY")
 # KRRN.forward replays a hipGraph of its plan (captured after one serial warm-up run): the only
 # form in which the plan's side streams run concurrently (runtime.Plan); 0 = serial eager runs
 GRAPH = knobs.flag("KRRN_GRAPH")
+# the fusion work that reads only the input cloud (the level-0 kNN and the v branch's level-0
+# convs) is emitted at the start of the forward on stream CLOUD_SID, beside the HRNet phase
+FUSION_EARLY = knobs.flag("KRRN_FUSION_EARLY")
 
 
 class KRRNPlan:
@@ -60,6 +63,7 @@ class KRRNPlan:
     # side stream of the pose step when it is fused into the forward plan (pose_hook)
     POSE_SID = 6
     TBASE_SID = 5  # TBase conv1's level-1 half (posenet.emit_tbase_level1)
+    CLOUD_SID = 7  # the fusion's cloud-only part (fusion.emit_fusion_cloud_part), joined before `split`
     POSE_AT = knobs.text("KRRN_POSE_AT")  # measured: level1 16.68, heads 16.80, level2 16.80 ms/step
 
     def __init__(self, model: "KRRN", B: int, S: int, N: int, opt_pose: bool, device, pose_hook=None,
@@ -84,7 +88,16 @@ class KRRNPlan:
         self.seed = torch.zeros(1, dtype=torch.int64, device=device)
         xa = Act(plan.buf((B, S, S, 4)), B, S, S, 4, 0, 3)
         plan.add("krrn_nchw_to_nhwc_f32", ptr(self.x_in), B, 3, S, S, ptr(xa.t), 4, 0)
+        early, early_ids = None, set()
+        if FUSION_EARLY and opt_pose:
+            plan.fork([self.CLOUD_SID])
+            e0 = len(plan.ops)
+            with plan.on_stream(self.CLOUD_SID):
+                early = emit_fusion_cloud_part(model.fusion, plan, B, N, self.cloud)
+            early_ids = {id(op) for op in plan.ops[e0:] if op.name != "sync"}
         xmap, ymap, specs = build_hrnet_plan(model.backbone, plan, xa)
+        if early is not None:
+            plan.join([self.CLOUD_SID])
         # ops[:split] = the backbone (all its side streams joined); ops[split:] read only xmap / ymap
         # of it (plus the static inputs), which lets BatchPipeline(pipelined=True) overlap a batch's
         # backbone with the previous batch's heads / fusion / pose
@@ -182,9 +195,10 @@ class KRRNPlan:
                 hooks["level1"].append(tracked(emit_tb_l1))
             f0 = len(plan.ops)
             feat, self.fusion_bufs = build_fusion_plan(model.fusion, plan, B, N, self.p9, self.perms, hooks=hooks,
-                                                       materialize=model.keep_fusion_feat)
+                                                       materialize=model.keep_fusion_feat, early=early)
             # the FusionNetLite launches (for the bench's fusion HBM roofline; hook ops excluded)
             self.fusion_op_ids = {id(op) for op in plan.ops[f0:] if id(op) not in side_ids and op.name != "sync"}
+            self.fusion_op_ids |= early_ids  # FusionNetLite launches emitted ahead of the backbone
             self.feat = feat
             fb = self.fusion_bufs
             levels = dict(fm5=fb["fm5"], feat1=fb["feat1"], feat2=fb["feat2"], nn1=fb["nn1"], nn2=fb["nn2"], N1=N1,
