@@ -544,13 +544,17 @@ class _Builder:
         return out
 
 
-def build_hrnet_plan(net: HRNet, plan: Plan, x: Act) -> Tuple[Act, Act, list]:
-    """Emit the HRNet forward (myhrnet.py:471-527) for input act `x`; returns (x_out @S/4, y_out @S/2)."""
+def build_hrnet_plan(net: HRNet, plan: Plan, x: Act, after_layer1=None) -> Tuple[Act, Act, list]:
+    """Emit the HRNet forward (myhrnet.py:471-527) for input act `x`; returns (x_out @S/4, y_out @S/2).
+    after_layer1(): called once the stem and layer1 are emitted (the caller forks side-stream work
+    there, beside the latency-bound branch stages rather than the chip-filling stem)."""
     bld = _Builder(plan, x.B)
     h = bld.conv(x, net.conv1, net.bn1, relu=True)
     h = bld.conv(h, net.conv2, net.bn2, relu=True)
     for blk in net.layer1:
         h = bld.bottleneck(h, blk)
+    if after_layer1 is not None:
+        after_layer1()
     ylist = [h]
     nstages = len(net.spec.stages)
     on_streams = False  # ylist[k] lives on plan stream k (the previous stage was not joined)

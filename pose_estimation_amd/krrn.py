@@ -88,14 +88,19 @@ class KRRNPlan:
         self.seed = torch.zeros(1, dtype=torch.int64, device=device)
         xa = Act(plan.buf((B, S, S, 4)), B, S, S, 4, 0, 3)
         plan.add("krrn_nchw_to_nhwc_f32", ptr(self.x_in), B, 3, S, S, ptr(xa.t), 4, 0)
-        early, early_ids = None, set()
-        if FUSION_EARLY and opt_pose:
+        fe = {}
+
+        def emit_cloud_part():
             plan.fork([self.CLOUD_SID])
             e0 = len(plan.ops)
             with plan.on_stream(self.CLOUD_SID):
-                early = emit_fusion_cloud_part(model.fusion, plan, B, N, self.cloud)
-            early_ids = {id(op) for op in plan.ops[e0:] if op.name != "sync"}
-        xmap, ymap, specs = build_hrnet_plan(model.backbone, plan, xa)
+                fe["early"] = emit_fusion_cloud_part(model.fusion, plan, B, N, self.cloud)
+            fe["ids"] = {id(op) for op in plan.ops[e0:] if op.name != "sync"}
+
+        # forked after the stem / layer1 (which fill the chip), beside the HRNet branch stages
+        xmap, ymap, specs = build_hrnet_plan(model.backbone, plan, xa,
+                                             after_layer1=emit_cloud_part if FUSION_EARLY and opt_pose else None)
+        early, early_ids = fe.get("early"), fe.get("ids", set())
         if early is not None:
             plan.join([self.CLOUD_SID])
         # ops[:split] = the backbone (all its side streams joined); ops[split:] read only xmap / ymap
