@@ -193,6 +193,15 @@ int krrn_conv3x3_wino_f32(const float* in, int in_cs, int in_co, int B, int H, i
 int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* U3,
                              int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                              int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
+/* The same conv by Winograd F(4x4, 3x3) (points 0, +-1, +-2; 2.25 products per output instead of
+ * 4) on split-bf16 operands, for the heads' wide 128 -> 128 convs (krrn.py:52-63, 74-81). U3 is
+ * wino4_weights' U = G g G^T ([cin/8][36][N][8] f32, element xi = 6u + v) split on the host
+ * (wino_weights_x3): plane U_mh [cin/8][36][N][2][8] bf16 then plane U_l [cin/8][36][N][2][4]
+ * bf16. cin a multiple of 8; in 16-byte aligned with in_cs, in_co multiples of 4; other arguments
+ * as krrn_conv3x3_wino_x3_f32 (any out / res channel alignment). */
+int krrn_conv3x3_wino4_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* U3,
+                              int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
+                              int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
 /* A head's last 3x3 conv fused with its final 1x1 conv (nml_final, krrn.py:80-84 / 98, when it has
  * at most 4 output channels): h = act(scale[n] * conv3x3 + bias[n] (+ res)) as
  * krrn_conv3x3_wino_x3_f32 with n_store = N, then out[b][o][y][x] = sum_n w1[o][n] h[n] + b1[o]

@@ -116,6 +116,7 @@ class _Emit:
 
     def __init__(self, fu: FusionNetLite, plan: Plan, B: int, keep: list):
         self.plan, self.B, self.dev, self.S, self.keep = plan, B, plan.device, fu.support_num, keep
+        self._lin: dict = {}
 
     def knn(self, q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, out):
         self.plan.add("krrn_knn_f32", q, q_bs, q_st, nq, qidx, c, c_bs, c_st, nc, d, k, drop, mode, self.B, ptr(out))
@@ -128,9 +129,14 @@ class _Emit:
                       int(relu), out, o_bs, o_st, self.B if Bc is None else Bc)
 
     def gemm(self, a, a_cs, a_co, M, layer: "Conv_layer", out):
-        spec = ops.make_linear(layer.weights.detach().t(), layer.bias, None, self.dev,
-                               cin_p=ops.pad4(layer.in_channel))
-        self.keep.append(spec)
+        # one spec per layer: a GEMM repeated over crop chunks shares its weights (and add_gemm its
+        # packed copy)
+        spec = self._lin.get(id(layer))
+        if spec is None:
+            spec = ops.make_linear(layer.weights.detach().t(), layer.bias, None, self.dev,
+                                   cin_p=ops.pad4(layer.in_channel))
+            self._lin[id(layer)] = spec
+            self.keep.append(spec)
         np_ = ops.pad4(spec.cout)
         if add_gemm(self.plan, a=a, a_off=a_co, lda=a_cs, M=M, wt=spec.wt[0], K=spec.cin_p, N=np_, scale=spec.scale,
                     bias=spec.bias, out=out, ldo=out.shape[-1], relu=False, cin=spec.cin, cout=spec.cout,

@@ -235,7 +235,12 @@ class _Builder:
         if out is None:
             out = self.act(Ho, Wo, spec.cout)
         assert (out.H, out.W) == (Ho, Wo) and out.cp >= pad4(spec.cout)
-        if ops.wino_eligible(spec, x.B * Ho * Wo) and x.cs % 2 == 0 and x.co % 2 == 0:
+        if (WINO_X3 and ops.wino_eligible(spec, x.B * Ho * Wo) and (Ho, Wo) == (x.H, x.W)
+                and ops.wino4_eligible(spec, x, Ho, Wo)):
+            U = ops.wino_weights_x3(ops.wino4_weights(conv, self.dev, cin_map=cin_map, cin_p=x.cp))
+            self.specs.append(U)
+            self.emit_wino4(x, spec, U, out, res, relu)
+        elif ops.wino_eligible(spec, x.B * Ho * Wo) and x.cs % 2 == 0 and x.co % 2 == 0:
             U = ops.wino_weights(conv, self.dev, cin_map=cin_map, cin_p=x.cp)
             if WINO_X3:
                 U = ops.wino_weights_x3(U)
@@ -348,6 +353,21 @@ class _Builder:
                       x.W, spec.cin_p, ptr(U), np_, np_, ptr(spec.scale), ptr(spec.bias),
                       ptr(res.t) if res is not None else ptr(None), res.cs if res is not None else 0,
                       res.co if res is not None else 0, ptr(out.t), out.cs, out.co, int(relu), meta=meta)
+
+    def emit_wino4(self, x: Act, spec, U: torch.Tensor, out: Act, res: Optional[Act], relu: bool,
+                   tag: str = "conv"):
+        """Fused Winograd F(4x4,3x3) on split-bf16 operands (krrn_conv3x3_wino4_x3_f32; U = the
+        wino_weights_x3 planes of wino4_weights)."""
+        np_ = pad4(spec.cout)
+        M = x.B * out.H * out.W
+        tiles = x.B * ((out.H + 3) // 4) * ((out.W + 3) // 4)
+        pipe = 2.0 * 36 * spec.cin_p * np_ * tiles  # f32-equivalent component products (see emit_wino)
+        meta = dict(kernel="wino_f43_x3", flops=2.0 * spec.cin * spec.cout * 9 * M, tag=tag + "_wino", M=M, N=np_,
+                    K=spec.cin_p * 9, mfma_flops=pipe * 6 / 16, mfma_bf16_flops=pipe * 6)
+        self.plan.add("krrn_conv3x3_wino4_x3_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(U), np_, np_,
+                      ptr(spec.scale), ptr(spec.bias), ptr(res.t) if res is not None else ptr(None),
+                      res.cs if res is not None else 0, res.co if res is not None else 0, ptr(out.t), out.cs,
+                      out.co, int(relu), meta=meta)
 
     def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         np_ = pad4(spec.cout)
@@ -565,6 +585,12 @@ def build_hrnet_plan(net: HRNet, plan: Plan, x: Act, after_layer1=None) -> Tuple
         # per-stream stages: every module of the stage chains per stream (the grouped form runs on
         # stream 0, so not with it)
         cross = STAGE_STREAMS and MODULE_STREAMS and not HR_GROUP and all(m.num_branches > 1 for m in stage)
+        if on_streams and not cross:
+            # the previous stage left branch k on stream k, but this stage runs its transitions on
+            # stream 0 and forks from it: join first (not reached with W18 / W32 / W48, where every
+            # stage after the first cross one is cross too; a custom spec with a 1-branch module is)
+            plan.join(list(range(1, len(ylist))))
+            on_streams = False
         xl = []
         for i in range(nb):
             t = trans[i]

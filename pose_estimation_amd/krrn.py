@@ -103,9 +103,14 @@ class KRRNPlan:
         early, early_ids = fe.get("early"), fe.get("ids", set())
         if early is not None:
             plan.join([self.CLOUD_SID])
-        # ops[:split] = the backbone (all its side streams joined); ops[split:] read only xmap / ymap
-        # of it (plus the static inputs), which lets BatchPipeline(pipelined=True) overlap a batch's
-        # backbone with the previous batch's heads / fusion / pose
+        # ops[:split] = the backbone (all its side streams joined) plus, with FUSION_EARLY, the
+        # fusion's cloud-only part (emit_fusion_cloud_part: idx0, F0, feat1 and Y1v, written on
+        # CLOUD_SID and joined above). ops[split:] read xmap / ymap, those early fusion buffers and
+        # the static inputs. PipelinedPipeline runs a slot's ops[:split] (stage A) and ops[split:]
+        # (stage B) as two graphs; it is correct only because every slot owns its plan buffers and a
+        # slot's stage A never runs beside its own stage B (stage A of batch k + 1 runs beside stage
+        # B of batch k, on the other slot's plan) -- two sub-plans of ONE slot must never run
+        # concurrently.
         self.split = len(plan.ops)
         self.backbone_out = (xmap.t, ymap.t)
         bld = _Builder(plan, B)

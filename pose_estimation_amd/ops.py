@@ -220,6 +220,10 @@ def make_conv(conv: torch.nn.Conv2d, bn: Optional[torch.nn.Module], device, cin_
     return ConvSpec([wt], [taps], [(0, 0)], scale, bias, cin_p, cout, s, "conv", k, pad, len(cin_map))
 
 
+# Winograd switches, read at import like every other knob (knobs.py)
+WINO = knobs.flag("KRRN_WINO")
+WINO4 = knobs.flag("KRRN_WINO4")
+
 # Winograd F(2x2, 3x3) weight transform G (Lavin & Gray 2016): U = G g G^T
 WINO_G = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]], dtype=torch.float64)
 
@@ -242,6 +246,30 @@ def wino_weights(conv: torch.nn.Conv2d, device, cin_map: Optional[List[int]] = N
     return out.float().contiguous().to(device)
 
 
+# Winograd F(4x4, 3x3) weight transform G, points (0, +-1, +-2) (Lavin & Gray 2016): U = G g G^T
+WINO4_G = torch.tensor([[1 / 4, 0.0, 0.0], [-1 / 6, -1 / 6, -1 / 6], [-1 / 6, 1 / 6, -1 / 6],
+                        [1 / 24, 1 / 12, 1 / 6], [1 / 24, -1 / 12, 1 / 6], [0.0, 0.0, 1.0]], dtype=torch.float64)
+
+
+def wino4_weights(conv: torch.nn.Conv2d, device, cin_map: Optional[List[int]] = None,
+                  cin_p: Optional[int] = None) -> torch.Tensor:
+    """[cout, cin, 3, 3] -> U f32 for krrn_conv3x3_wino4_x3_f32 in chunk-major order
+    [ceil(cin_p/8)][36][pad4(cout)][8] (xi = 6u + v; channels past cin_p are zero), transformed in
+    f64 (G's 1/6 and 1/24 are not exact in f32; the f32 rounding of U happens once, here)."""
+    w = conv.weight.detach().cpu().double()
+    cout, cin = w.shape[:2]
+    if cin_map is None:
+        cin_map = list(range(cin))
+    cin_p = pad4(max(cin_map) + 1) if cin_p is None else cin_p
+    u = torch.einsum("ui,ncij,vj->uvnc", WINO4_G, w, WINO4_G)  # [6, 6, cout, cin]
+    out = torch.zeros(36, pad4(cout), cin_p, dtype=torch.float64)
+    out[:, :cout, torch.tensor(cin_map, dtype=torch.long)] = u.reshape(36, cout, cin)
+    nck = (cin_p + 7) // 8
+    out = torch.nn.functional.pad(out, (0, 8 * nck - cin_p))
+    out = out.view(36, pad4(cout), nck, 8).permute(2, 0, 1, 3)  # [chunk][xi][n][8]
+    return out.float().contiguous().to(device)
+
+
 def split_bf16x3(u: torch.Tensor):
     """f32 -> three bf16 terms, each the round-to-nearest of what the previous ones left:
     u = h + m + l exactly (24 significand bits), |m| <= 2^-8 |u|, |l| <= 2^-16 |u|."""
@@ -254,12 +282,13 @@ def split_bf16x3(u: torch.Tensor):
 
 
 def wino_weights_x3(U: torch.Tensor) -> torch.Tensor:
-    """wino_weights' U [nck][16][N][8] f32 -> the split planes krrn_conv3x3_wino_x3_f32 reads, as
-    one bf16 tensor: U_mh [nck][16][N][half][m0..m3 h0..h3] then U_l [nck][16][N][half][l0..l3]
+    """wino_weights' U [nck][16][N][8] (or wino4_weights' [nck][36][N][8]) f32 -> the split planes
+    krrn_conv3x3_wino_x3_f32 (krrn_conv3x3_wino4_x3_f32) reads, as one bf16 tensor:
+    U_mh [nck][xi][N][half][m0..m3 h0..h3] then U_l [nck][xi][N][half][l0..l3]
     (half = channels 4 half .. 4 half + 3 of the chunk)."""
     h, m, l = split_bf16x3(U)
-    nck, _, N, _ = U.shape
-    h, m, l = (t.reshape(nck, 16, N, 2, 4) for t in (h, m, l))
+    nck, nxi, N, _ = U.shape
+    h, m, l = (t.reshape(nck, nxi, N, 2, 4) for t in (h, m, l))
     mh = torch.cat([m, h], dim=-1).reshape(-1)
     return torch.cat([mh, l.reshape(-1)]).contiguous()
 
@@ -326,10 +355,22 @@ def gemm_weights_panel(wt: torch.Tensor) -> torch.Tensor:
 def wino_eligible(spec: ConvSpec, M: int) -> bool:
     """Fused Winograd for the wide stride-1 3x3 convs (>= 32 channels in and out, >= 32k output
     pixels); the narrow HRNet branches stay on the implicit GEMM (latency-bound there)."""
-    if not knobs.flag("KRRN_WINO"):
+    if not WINO:
         return False
     return (spec.kind == "conv" and spec.ksize == 3 and spec.stride == 1 and spec.pad == 1
             and spec.cin_p >= 32 and spec.cout >= 32 and M >= 32768)
+
+
+def wino4_eligible(spec: ConvSpec, x, H: int, W: int) -> bool:
+    """Winograd F(4x4, 3x3) (krrn_conv3x3_wino4_x3_f32) for the heads' wide 128 -> 128 convs: a
+    wino-eligible conv with >= 64 input channels (a multiple of 8), >= 64 outputs and a map of at
+    least 32 x 32, whose NHWC input is 16-byte aligned. The narrower / smaller Winograd convs (layer1
+    and last_layer at S/4, 64 / 272 channels at 30 x 30) keep F(2x2): measured per shape,
+    DESIGN.md section 3."""
+    if not WINO4:
+        return False
+    return (spec.cin_p % 8 == 0 and spec.cin_p >= 64 and spec.cout >= 64 and min(H, W) >= 32
+            and x.cs % 4 == 0 and x.co % 4 == 0)
 
 
 def small_conv_config(M: int, ntiles: int, cin_p: int):

@@ -48,6 +48,7 @@ _lib.register("krrn_conv2d_x3_f32", [P, I, I, I, I, I, I, I, I, I, I, P, P, P, I
                                      I, I, I, I, I, I, I, P, P])
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv3x3_wino_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
+_lib.register("krrn_conv3x3_wino4_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv3x3_wino_x3_head_f32", [P, I, I, I, I, I, I, P, I, P, P, P, I, I, I, P, P, I, P, P, I, P])
 _lib.register("krrn_conv1x1_nchw_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
 _lib.register("krrn_conv1x1_nchw_x3_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
@@ -182,6 +183,7 @@ class Plan:
         self.nstreams = 1
         self._side: List[torch.cuda.Stream] = []
         self._scratch: Dict[Tuple[int, int], torch.Tensor] = {}
+        self._packed: Dict[tuple, torch.Tensor] = {}  # packed GEMM weights, shared by repeated GEMMs
 
     def buf(self, shape, dtype=torch.float32, zero: bool = True) -> torch.Tensor:
         t = (torch.zeros if zero else torch.empty)(tuple(shape), dtype=dtype, device=self.device)
@@ -488,11 +490,20 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
     if scale is not None:
         w = w * scale.reshape(N, 1).to(w.device)
     w = w.contiguous()
+    wkey = (wt.data_ptr(), scale.data_ptr() if scale is not None else 0, K, N)
+
+    def packed(kind: str, fn):
+        """The kernel's packed weights, built once per (weights, scale, kind) in a plan: a GEMM
+        repeated over row chunks (the fusion's level-0 crop chunks) shares one copy."""
+        key = wkey + (kind,)
+        if key not in plan._packed:
+            plan._packed[key] = fn(w)
+            plan.buffers.append([plan._packed[key], bias])
+        return plan._packed[key]
     flops = 2.0 * (cin or K) * (cout or N) * M * batch
     if GEMM_PANEL and not require_x3 and K in (64, 128) and N % 32 == 0 and N <= 2048 and batch == 1 \
             and lda % 4 == 0 and a_off % 4 == 0 and not (K == 128 and res is not None):
-        wp = ops.gemm_weights_panel(w)
-        plan.buffers.append([wp, bias])
+        wp = packed("panel", ops.gemm_weights_panel)
         csplit = 1
         tiles = N // 32
         if K == 128:
@@ -516,8 +527,7 @@ def add_gemm(plan: Plan, *, a: torch.Tensor, a_off: int, lda: int, M: int, wt: t
     if GEMM_X3 and K >= GEMM_X3_MINK and K % 32 == 0 and N % 128 == 0 and lda % 4 == 0 and ldo % 4 == 0 and a_off % 4 == 0 \
             and (res is None or ldr % 4 == 0):
         # own split-bf16 GEMM (gemm_x3.hip): 6 bf16 term products per f32 product
-        w3 = ops.gemm_weights_x3(w)
-        plan.buffers.append([w3, bias])
+        w3 = packed("x3", ops.gemm_weights_x3)
         plan.add("krrn_gemm_x3_f32", P(a.data_ptr() + 4 * a_off), lda, M, K, N, ptr(w3), ptr(bias), ptr(res), ldr,
                  ptr(out), ldo, int(relu), batch, a_grp, o_grp, r_grp,
                  meta=dict(kernel="gemm_x3", flops=flops, tag=tag, M=M * batch, N=N, K=K, splits=1,

@@ -1,8 +1,9 @@
-"""Micro-bench: krrn_conv3x3_wino_f32 (f32 MFMA) against krrn_conv3x3_wino_x3_f32 (split-bf16
-MFMA) on the step's Winograd shapes: time per launch, and the error of each
-against an f64 CPU conv of the first 2 images (max |err| / max |ref| and RMS err / RMS ref).
+"""Micro-bench: krrn_conv3x3_wino_f32 (f32 MFMA), krrn_conv3x3_wino_x3_f32 (split-bf16 F(2x2,3x3))
+and krrn_conv3x3_wino4_x3_f32 (split-bf16 F(4x4,3x3)) on the step's Winograd shapes: time per launch,
+and the error of each against an f64 CPU conv of the first 2 images (max |err| / max |ref| and RMS
+err / RMS ref).
 
-usage (GPU box): python3 profiles/bench_wino_x3.py
+usage (GPU box): python3 profiles/bench_wino_x3.py      (KERNELS=x3,w4 selects; REPS=n)
 """
 import os
 import sys
@@ -43,6 +44,7 @@ for B, cin, cout, H, W in shapes:
     xa.t.copy_(x.permute(0, 2, 3, 1).to(dev))
     U = ops.wino_weights(conv, dev, cin_p=cin)
     U3 = ops.wino_weights_x3(U)
+    U4 = ops.wino_weights_x3(ops.wino4_weights(conv, dev, cin_p=cin)) if cin % 8 == 0 else None
     out = ops.new_act(B, H, W, cout, dev, cs=cout)
     st = P(torch.cuda.current_stream().cuda_stream)
     with torch.no_grad():
@@ -57,11 +59,18 @@ for B, cin, cout, H, W in shapes:
         _lib.check(L.krrn_conv3x3_wino_x3_f32(ptr(xa.t), xa.cs, 0, B, H, W, cin, ptr(U3), cout, cout, ptr(None),
                                               ptr(None), ptr(None), 0, 0, ptr(out.t), out.cs, 0, 0, st), "wino_x3")
 
+    def w4():
+        _lib.check(L.krrn_conv3x3_wino4_x3_f32(ptr(xa.t), xa.cs, 0, B, H, W, cin, ptr(U4), cout, cout, ptr(None),
+                                               ptr(None), ptr(None), 0, 0, ptr(out.t), out.cs, 0, 0, st), "wino4_x3")
+
     fl = 2.0 * B * H * W * cin * cout * 9
     line = f"B{B} {cin}->{cout} {H}x{W}:"
-    for name, fn in (("f32", f32), ("x3", x3)):
+    kinds = os.environ.get("KERNELS", "f32,x3,w4").split(",")
+    for name, fn in (("f32", f32), ("x3", x3), ("w4", w4)):
+        if name not in kinds or (name == "w4" and U4 is None):
+            continue
         out.t.zero_()
-        ms = ev_time(fn)
+        ms = ev_time(fn, int(os.environ.get("REPS", "10")))
         line += f" | {name} {ms * 1e3:7.1f} us {fl / ms / 1e9:6.1f} TF(alg)"
         if ref is not None:
             e = out.t[:2, :, :, :cout].double().cpu() - ref

@@ -342,6 +342,54 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     torch.testing.assert_close(got3, got, rtol=1e-5, atol=2e-6 * scale)
 
 
+@pytest.mark.parametrize("cin,cout,H,W,co,relu", [(128, 128, 32, 40, 0, 1), (64, 72, 33, 37, 4, 1),
+                                                  (96, 128, 35, 64, 8, 0), (128, 64, 60, 60, 0, 1),
+                                                  (128, 128, 120, 120, 0, 1)])
+def test_conv3x3_winograd4(dev, cin, cout, H, W, co, relu):
+    """Fused Winograd F(4x4,3x3) on split-bf16 operands (krrn_conv3x3_wino4_x3_f32): ragged tiles (H, W
+    not multiples of 4 or of a block's 64 x 8 pixels), channel-offset input / output, residual, BN.
+    vs torch fp32 (TOL) and vs an f64 conv: max |err| <= 1e-5 max |ref|. F(4x4)'s transform constants
+    (up to 25 in B^T B, 8 in A^T, 1/24 in G) make its rounding error ~6x F(2x2)'s (RMS 7.4e-7 vs 1.2e-7
+    of max|ref| in the round-5 CPU study); the f32 conv's own error is ~3e-7."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, ptr
+    g = torch.Generator().manual_seed(cin + cout + H + W)
+    B = 3 if H * W < 10000 else 2
+    conv = nn.Conv2d(cin, cout, 3, 1, 1, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / (3.0 * cin ** 0.5))
+        conv.bias.copy_(0.1 * torch.randn(cout, generator=g))
+    bn = _bn(cout, g)
+    x = torch.relu(torch.randn(B, cin, H, W, generator=g))
+    res = torch.randn(B, cout, H, W, generator=g)
+    act = torch.relu if relu else (lambda t: t)
+    ref = act(bn(conv(x)) + res).detach()
+    with torch.no_grad():
+        s64 = (bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps))
+        y64 = F.conv2d(x.double(), conv.weight.double(), conv.bias.double(), padding=1)
+        ref64 = act((y64 - bn.running_mean.double()[:, None, None]) * s64[:, None, None]
+                    + bn.bias.double()[:, None, None] + res.double())
+    cs = ops.pad4(cin) + co + 4
+    xa = _nhwc(x, dev, cs=cs, co=co)
+    spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
+    U3 = ops.wino_weights_x3(ops.wino4_weights(conv, dev, cin_p=ops.pad4(cin)))
+    ra = _nhwc(res, dev)
+    np_ = ops.pad4(cout)
+    out = ops.new_act(B, H, W, cout, dev, cs=np_ + co + 4)
+    out.t.fill_(7.0)
+    L = _lib.lib()
+    _lib.check(L.krrn_conv3x3_wino4_x3_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_, np_,
+                                           ptr(spec.scale), ptr(spec.bias), ptr(ra.t), ra.cs, 0, ptr(out.t), out.cs,
+                                           co, relu, P(torch.cuda.current_stream().cuda_stream)), "wino4")
+    torch.cuda.synchronize()
+    t = out.t.cpu()
+    got = t[..., co:co + cout].permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, **TOL)
+    err = float((got.double() - ref64).abs().max() / ref64.abs().max())
+    assert err <= 1e-5, err
+    assert torch.all(t[..., :co] == 7.0) and torch.all(t[..., co + np_:] == 7.0)
+
+
 @pytest.mark.parametrize("cin,cout,H,W,co,p1,with_res", [
     (128, 128, 120, 120, 0, 3, False), (64, 72, 17, 23, 4, 4, True), (20, 132, 9, 8, 0, 1, True),
     (36, 40, 7, 9, 8, 2, False)])
