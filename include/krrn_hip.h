@@ -202,6 +202,12 @@ int krrn_conv3x3_wino_x3_f32(const float* in, int in_cs, int in_co, int B, int H
 int krrn_conv3x3_wino4_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin, const void* U3,
                               int N, int n_store, const float* scale, const float* bias, const float* res, int res_cs,
                               int res_co, float* out, int out_cs, int out_co, int relu, void* stream);
+/* krrn_conv3x3_wino_x3_head_f32 on the F(4x4, 3x3) kernel (U3 as krrn_conv3x3_wino4_x3_f32; cin a
+ * multiple of 8, in 16-byte aligned with in_cs, in_co multiples of 4). */
+int krrn_conv3x3_wino4_x3_head_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
+                                   const void* U3, int N, const float* scale, const float* bias, const float* res,
+                                   int res_cs, int res_co, int relu, const float* w1, const float* b1, int p1,
+                                   float* part, float* out, int out_c, void* stream);
 /* A head's last 3x3 conv fused with its final 1x1 conv (nml_final, krrn.py:80-84 / 98, when it has
  * at most 4 output channels): h = act(scale[n] * conv3x3 + bias[n] (+ res)) as
  * krrn_conv3x3_wino_x3_f32 with n_store = N, then out[b][o][y][x] = sum_n w1[o][n] h[n] + b1[o]
@@ -227,23 +233,6 @@ int krrn_conv_small_f32(const float* in, int in_cs, int in_co, int B, int H, int
                         int n_store, const float* scale, const float* bias, const float* res, int res_cs, int res_co,
                         float* out, int out_cs, int out_co, int relu, int ksize, int stride, int nw, int ks,
                         void* stream);
-/* The arguments of krrn_conv_small_f32 as a struct, and up to 4 independent such convs in ONE
- * launch (e.g. the j-th BasicBlock conv of every HRNet branch, myhrnet.py:177-231: the branches
- * are independent until the fuse layer). Each problem computes exactly what krrn_conv_small_f32
- * computes with the same arguments (bit-identical). */
-typedef struct krrn_small_desc {
-  const float* in;
-  int in_cs, in_co, B, H, W, cin;
-  const float* wt;
-  int N, n_store;
-  const float* scale;
-  const float* bias;
-  const float* res;
-  int res_cs, res_co;
-  float* out;
-  int out_cs, out_co, relu, ksize, stride, nw, ks;
-} krrn_small_desc;
-int krrn_conv_small_group_f32(const krrn_small_desc* descs, int n, void* stream);
 
 
 /* k nearest neighbours without the [n, n] distance matrix.

@@ -253,39 +253,6 @@ __global__ __launch_bounds__(256) void conv_small_kernel(const SmallArgs a) {
   small_body<NW, KS>(a, blockIdx.x, blockIdx.y, slab);
 }
 
-// Up to 4 independent problems (the j-th BasicBlock conv of every HRNet branch) in one launch:
-// block b belongs to the problem whose [start, start + blocks) range holds it, and runs that
-// problem's (NW, KS) body on its (m-block, n-block) exactly as the single launch would (the
-// same instructions per output: bit-identical results). Problems are ordered longest block first.
-constexpr int kSmallMaxGroup = 4;
-struct SmallGroup {
-  SmallArgs a[kSmallMaxGroup];
-  int cfg[kSmallMaxGroup];  // (nw - 1) + 3 * log2(ks)
-  int gx[kSmallMaxGroup];   // m-blocks
-  int start[kSmallMaxGroup + 1];
-  int n;
-};
-
-__global__ __launch_bounds__(256) void conv_small_group_kernel(const SmallGroup g) {
-  extern __shared__ __attribute__((aligned(16))) float slab[];
-  const int blk = blockIdx.x;
-  int i = 0;
-  while (i + 1 < g.n && blk >= g.start[i + 1]) ++i;
-  const int r = blk - g.start[i];
-  const int by = r / g.gx[i], bx = r - by * g.gx[i];
-  switch (g.cfg[i]) {
-    case 0: small_body<1, 1>(g.a[i], bx, by, slab); break;
-    case 1: small_body<2, 1>(g.a[i], bx, by, slab); break;
-    case 2: small_body<3, 1>(g.a[i], bx, by, slab); break;
-    case 3: small_body<1, 2>(g.a[i], bx, by, slab); break;
-    case 4: small_body<2, 2>(g.a[i], bx, by, slab); break;
-    case 5: small_body<3, 2>(g.a[i], bx, by, slab); break;
-    case 6: small_body<1, 4>(g.a[i], bx, by, slab); break;
-    case 7: small_body<2, 4>(g.a[i], bx, by, slab); break;
-    default: small_body<3, 4>(g.a[i], bx, by, slab); break;
-  }
-}
-
 // LDS floats of the largest slab any block of this problem stages (host mirror of the kernel's
 // row count: the input rows of the output rows a block's pixel range covers)
 long long slab_floats(const SmallArgs& a, int pixb) {
@@ -383,49 +350,3 @@ KRRN_API int krrn_conv_small_f32(const float* in, int in_cs, int in_co, int B, i
   return KRRN_EARG;
 }
 
-KRRN_API int krrn_conv_small_group_f32(const krrn_small_desc* d, int n, void* stream) {
-  if (!d || n < 1 || n > kSmallMaxGroup) return KRRN_EARG;
-  SmallGroup g;
-  long long blocks[kSmallMaxGroup], lds = 0;
-  int order[kSmallMaxGroup];
-  for (int i = 0; i < n; ++i) {
-    SmallArgs& a = g.a[i];
-    const krrn_small_desc& q = d[i];
-    const int st = make_args(q.in, q.in_cs, q.in_co, q.B, q.H, q.W, q.cin, q.wt, q.N, q.n_store, q.scale, q.bias,
-                             q.res, q.res_cs, q.res_co, q.out, q.out_cs, q.out_co, q.relu, q.ksize, q.stride, q.nw,
-                             q.ks, a);
-    if (st != KRRN_OK) return st;
-    const long long l = small_lds(a, q.nw, q.ks);
-    if (l > lds) lds = l;
-    order[i] = i;
-  }
-  // longest block first: per-block MFMA steps ~ ceil(9 cin / 16) / ks x nw tiles
-  auto cost = [&](int i) {
-    return (long long)((d[i].ksize * d[i].ksize * d[i].cin + 15) / 16 + d[i].ks - 1) / d[i].ks * d[i].nw;
-  };
-  for (int i = 1; i < n; ++i)
-    for (int j = i; j > 0 && cost(order[j]) > cost(order[j - 1]); --j) {
-      const int t = order[j];
-      order[j] = order[j - 1];
-      order[j - 1] = t;
-    }
-  SmallGroup h;
-  h.n = n;
-  long long total = 0;
-  for (int r = 0; r < n; ++r) {
-    const int i = order[r];
-    const krrn_small_desc& q = d[i];
-    h.a[r] = g.a[i];
-    h.cfg[r] = (q.nw - 1) + 3 * (q.ks == 1 ? 0 : (q.ks == 2 ? 1 : 2));
-    h.gx[r] = krrn_cdiv(g.a[i].M, 64 / q.ks);
-    blocks[r] = (long long)h.gx[r] * krrn_cdiv(krrn_cdiv(q.N, 16), q.nw);
-    h.start[r] = (int)total;
-    total += blocks[r];
-  }
-  h.start[n] = (int)total;
-  if (total > 0x7fffffffLL) return KRRN_ESHAPE;
-  const int st = set_lds((const void*)conv_small_group_kernel, lds);
-  if (st != KRRN_OK) return st;
-  hipLaunchKernelGGL(conv_small_group_kernel, dim3((unsigned)total), dim3(256), (size_t)lds, (hipStream_t)stream, h);
-  return krrn_launch_status();
-}

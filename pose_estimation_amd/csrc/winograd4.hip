@@ -39,6 +39,8 @@
 //   Epilogue: 4 rounds of 8 tiles: each wave writes its accumulators to LDS as [comp][n][tile], then
 //   thread (n, tile quad, output row i) forms t[v] = A_i(M[.][v]) and Y[i][j] = A_j(t), applies
 //   BN / bias / residual / ReLU and stores: lanes run over channels (256-B store runs).
+#include <type_traits>
+
 #include "krrn_common.h"
 
 namespace {
@@ -59,12 +61,18 @@ constexpr int kRing = 1536;                       // slots per ring slot (10 x 1
 constexpr int kRingF = kRing * 4;                 // floats per ring slot
 constexpr int kVMH = 36 * 64 * 4;                 // u32 per V buffer, plane [V_m V_h]
 constexpr int kVL = 36 * 64 * 2;                  // u32 per V buffer, plane [V_l]
-constexpr int kEQ = kN * 4 * 4;                   // epilogue bytes per (component, tile quad): [n][4 tiles]
+constexpr int kET = kN * 4;                       // epilogue bytes per (component, tile): [64 n] f32
 constexpr unsigned kOOB = 0xFFFF0000u;
 // timing experiments only (results wrong; profiles/build_variant.sh): 1 no MFMAs, 2 no weight reloads,
 // 3 no transform, 4 no raw staging after the prologue, 5 no epilogue
 #ifndef KRRN_W4_EXP
 #define KRRN_W4_EXP 0
+#endif
+#ifndef KRRN_W4_RAWK
+#define KRRN_W4_RAWK 6  // component slot after which the next raw chunk is loaded
+#endif
+#ifndef KRRN_W4_GAP
+#define KRRN_W4_GAP 6  // transform VALU instructions placed in each MFMA gap
 #endif
 static_assert(kRR * kRS <= kRing && kRing == 3 * 512, "raw ring");
 static_assert(2 * (kRC - 1) + 1 + (kRC - 1) / 4 < kRS && (kRS * 4) % 16 == 0, "padded raw row");
@@ -73,7 +81,7 @@ static_assert(2 * (kRC - 1) + 1 + (kRC - 1) / 4 < kRS && (kRS * 4) % 16 == 0, "p
 constexpr int kOffL = 2 * kVMH * 4;              // 73728
 constexpr int kOffR = kOffL + 2 * kVL * 4;       // 110592
 constexpr int kLdsBytes = kOffR + 2 * kRingF * 4;  // 159744
-static_assert(36 * 4 * kEQ <= kLdsBytes, "epilogue (16 tiles) fits the LDS");
+static_assert(36 * 16 * kET <= kLdsBytes, "epilogue (16 tiles) fits the LDS");
 
 struct Wino4Args {
   const float* in;
@@ -89,8 +97,24 @@ struct Wino4Args {
   float* out;
   int out_cs, out_co;
   int relu;
+  int vec;          // out / res / scale / bias allow float4 channel runs
   int Ht, Wt;       // tiles per column / row
+  // head form (krrn_conv3x3_wino4_x3_head_f32): the activated conv output is not stored; its dot with
+  // the 4 rows of w1 ([4][N], the following 1x1 conv) over this block's 64 channels goes to
+  // part[nb][pixel][4], summed over the n-blocks in order by wino4_head_finish_kernel
+  const float* w1;
+  float* part;
 };
+
+// sum over the 16 lanes of a DPP row (every lane gets the sum): quad swaps, then half-row and row
+// mirrors (winograd.hip's head epilogue)
+__device__ __forceinline__ float row16_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));  // quad [1 0 3 2]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));  // quad [2 3 0 1]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));  // row_mirror
+  return x;
+}
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));  // RNE
@@ -151,91 +175,118 @@ __device__ __forceinline__ constexpr bool at_uses(int u) {
   return I == 0 ? (u <= 4) : (I == 3 ? (u >= 1) : (u >= 1 && u <= 4));
 }
 
-// T: column v of the transform for lane (tile, h): ring slot `ring` -> V buffer (vmh, vl). The
-// empty asm statements order the work (one patch row's reads at a time, one component's split and
-// store at a time): left alone, LLVM hoists every read and every split ahead of the stores and the
-// kernel spills (its accumulators and weights already take ~170 of the 256 registers).
-template <int V>
-__device__ __forceinline__ void transform(const char* rb, char* vm, char* vlo) {
-  // rb: this lane's patch origin in the ring slot; vm / vlo: this lane's V entry of component 0
-  auto rd = [&](int r, int c) {
-    return *reinterpret_cast<const f32x4*>(rb + 16 * (r * kRS + 2 * c + (c >> 2)));
-  };
-  auto row = [&](int r) {
-    f32x4 d[6];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) d[c] = bt_uses<V>(c) ? rd(r, c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    return bt_row<V>(d);
-  };
-  f32x4 e[6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    e[r] = row(r);
-    asm volatile("" : "+v"(e[r])::"memory");
-  }
-#pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    f32x4 x;
-    switch (u) {
-      case 0: x = bt_row<0>(e); break;
-      case 1: x = bt_row<1>(e); break;
-      case 2: x = bt_row<2>(e); break;
-      case 3: x = bt_row<3>(e); break;
-      case 4: x = bt_row<4>(e); break;
-      default: x = bt_row<5>(e); break;
-    }
-    const u32x6 ch = split3(x);
-    *reinterpret_cast<u32x4*>(vm + (6 * u + V) * 1024) = u32x4{ch[0], ch[1], ch[2], ch[3]};
-    *reinterpret_cast<u32x2*>(vlo + (6 * u + V) * 512) = u32x2{ch[4], ch[5]};
-    asm volatile("" : "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]), "+v"(e[4]), "+v"(e[5])::"memory");
-  }
-}
-
-// epilogue: output row I of the 4 tiles 16 pass + 4 tq .. + 3 (one f32x4 over the tiles), channel n;
-// E = [36][4 tile quads][64 n][4 tiles] f32 holds the pass's 16 tiles
-template <int I>
-__device__ __forceinline__ void epi_row(const Wino4Args& a, const char* E, int n, int tq, int pass, int b, int ty0,
-                                        int tx0, int ng) {
-  const char* eb = E + tq * (64 * 16) + n * 16;
+// epilogue: output row I of local tile tl (of the pass's 16), channels ng .. ng + 3;
+// E = [36][16 tiles][64 n] f32
+template <int I, bool HEAD>
+__device__ __forceinline__ void epi_row(const Wino4Args& a, const char* E, int nq, int tl, int pass, int b, int ty0,
+                                        int tx0, int ng, int nb) {
+  const char* eb = E + tl * kET + nq * 16;
   f32x4 t[6];
 #pragma unroll
   for (int v = 0; v < 6; ++v) {
     f32x4 m[6];
 #pragma unroll
     for (int u = 0; u < 6; ++u)
-      m[u] = at_uses<I>(u) ? *reinterpret_cast<const f32x4*>(eb + (6 * u + v) * kEQ * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      m[u] = at_uses<I>(u) ? *reinterpret_cast<const f32x4*>(eb + (6 * u + v) * 16 * kET) : f32x4{0.f, 0.f, 0.f, 0.f};
     t[v] = at_row<I>(m);
     asm volatile("" : "+v"(t[v])::"memory");  // one column's reads at a time (register budget)
   }
-  f32x4 y[4];  // y[j][q]: output column j of tile q
+  f32x4 y[4];  // y[j]: output column j, 4 channels
   y[0] = at_row<0>(t);
   y[1] = at_row<1>(t);
   y[2] = at_row<2>(t);
   y[3] = at_row<3>(t);
-  if (ng >= a.n_store) return;
-  const float scl = a.scale ? a.scale[ng] : 1.f;
-  const float bia = a.bias ? a.bias[ng] : 0.f;
+  const int tile = 16 * pass + tl;
+  const int ty = ty0 + (tile >> 4), tx = tx0 + (tile & 15);
+  const int oy = 4 * ty + I;
+  const int nj = min(4, a.W - 4 * tx);  // output columns of this tile inside the image
+  if constexpr (HEAD) {
+    // the 16 lanes of a DPP row are the 16 channel quads of one tile: every lane takes part in the
+    // row sums (no early exit), invalid pixels / channels contribute zeros
+    const bool ok = ty < a.Ht && oy < a.H && nj > 0 && ng < a.n_store;  // n_store = N % 4 == 0
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 scl = ok && a.scale ? *reinterpret_cast<const f32x4*>(a.scale + ng) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 bia = ok && a.bias ? *reinterpret_cast<const f32x4*>(a.bias + ng) : zero;
+    f32x4 w[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int tile = 16 * pass + 4 * tq + q;
-    const int ty = ty0 + (tile >> 4), tx = tx0 + (tile & 15);
-    const int oy = 4 * ty + I;
-    const int nj = min(4, a.W - 4 * tx);  // output columns of this tile inside the image
-    if (ty >= a.Ht || oy >= a.H || nj <= 0) continue;
+    for (int o = 0; o < 4; ++o) w[o] = ok ? *reinterpret_cast<const f32x4*>(a.w1 + (size_t)o * a.N + ng) : zero;
     const long long pix = ((long long)b * a.H + oy) * a.W + 4 * tx;
-    float* o = a.out + pix * a.out_cs + a.out_co + ng;
-    const float* rs = a.res ? a.res + pix * a.res_cs + a.res_co + ng : nullptr;
+    float sum[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool okj = ok && j < nj;
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(y[j][e], scl[e], bia[e]);
+      if (a.res && okj) v += *reinterpret_cast<const f32x4*>(a.res + (pix + j) * a.res_cs + a.res_co + ng);
+      if (a.relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (!okj) v = zero;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) sum[j][o] = row16_sum(v[0] * w[o][0] + v[1] * w[o][1] + v[2] * w[o][2] + v[3] * w[o][3]);
+    }
+    if (nq != 0 || !(ty < a.Ht && oy < a.H && nj > 0)) return;
+    const long long M = (long long)a.B * a.H * a.W;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < nj)
+        *reinterpret_cast<f32x4*>(a.part + ((size_t)nb * M + pix + j) * 4) = f32x4{sum[j][0], sum[j][1], sum[j][2], sum[j][3]};
+    return;
+  }
+  if (ty >= a.Ht || oy >= a.H || nj <= 0 || ng >= a.n_store) return;
+  const long long pix = ((long long)b * a.H + oy) * a.W + 4 * tx;
+  float* o = a.out + pix * a.out_cs + a.out_co + ng;
+  const float* rs = a.res ? a.res + pix * a.res_cs + a.res_co + ng : nullptr;
+  if (a.vec && ng + 4 <= a.n_store) {
+    const f32x4 scl = a.scale ? *reinterpret_cast<const f32x4*>(a.scale + ng) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 bia = a.bias ? *reinterpret_cast<const f32x4*>(a.bias + ng) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j >= nj) break;
-      float v = __builtin_fmaf(y[j][q], scl, bia);
-      if (rs) v += rs[j * a.res_cs];
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(y[j][e], scl[e], bia[e]);
+      if (rs) v += *reinterpret_cast<const f32x4*>(rs + j * a.res_cs);
+      if (a.relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      *reinterpret_cast<f32x4*>(o + j * a.out_cs) = v;
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (ng + e >= a.n_store) break;
+    const float scl = a.scale ? a.scale[ng + e] : 1.f, bia = a.bias ? a.bias[ng + e] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j >= nj) break;
+      float v = __builtin_fmaf(y[j][e], scl, bia);
+      if (rs) v += rs[j * a.res_cs + e];
       if (a.relu) v = fmaxf(v, 0.f);
-      o[j * a.out_cs] = v;
+      o[j * a.out_cs + e] = v;
     }
   }
 }
 
+// out[b][o][p] = sum over n-blocks (in order) of part[nb][b * HW + p][o] + b1[o], o < p1
+__global__ __launch_bounds__(256) void wino4_head_finish_kernel(const float* __restrict__ part, int nbn, long long M,
+                                                                int HW, const float* __restrict__ b1, int p1,
+                                                                float* __restrict__ out, int out_c) {
+  const long long m = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  f32x4 v = *reinterpret_cast<const f32x4*>(part + m * 4);
+  for (int nb = 1; nb < nbn; ++nb) v += *reinterpret_cast<const f32x4*>(part + ((size_t)nb * M + m) * 4);
+  const long long b = m / HW, p = m - b * HW;
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+    if (o < p1) out[(b * out_c + o) * HW + p] = v[o] + (b1 ? b1[o] : 0.f);
+}
+
+template <bool HEAD>
 __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -276,26 +327,6 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     for (int i = 0; i < 3; ++i) *reinterpret_cast<f32x4*>(dst + 8192 * i) = raw[i];
   };
 
-  // T: wave v < 6 transforms column v for lane (tile, h); its patch origin slot
-  const int ttile = lane & 31, th = lane >> 5;
-  const int pbase = (4 * (ttile >> 4)) * kRS + 9 * (ttile & 15) + th;
-  auto do_transform = [&](int ck) {
-    if (ck >= nck || KRRN_W4_EXP == 3) return;
-    const int p = ck & 1;
-    const char* rb = smem + kOffR + p * (kRingF * 4) + 16 * pbase;
-    char* vm = smem + p * (kVMH * 4) + 16 * lane;
-    char* vlo = smem + kOffL + p * (kVL * 4) + 8 * lane;
-    switch (wave) {
-      case 0: transform<0>(rb, vm, vlo); break;
-      case 1: transform<1>(rb, vm, vlo); break;
-      case 2: transform<2>(rb, vm, vlo); break;
-      case 3: transform<3>(rb, vm, vlo); break;
-      case 4: transform<4>(rb, vm, vlo); break;
-      case 5: transform<5>(rb, vm, vlo); break;
-      default: break;
-    }
-  };
-
   // M: wave (g, nh), components (u, v) = (3 (g >> 1) + k / 3, 3 (g & 1) + k % 3), k = 0..8
   const int g = wave & 3, nh = wave >> 2;
   const int cu0 = 3 * (g >> 1), cv0 = 3 * (g & 1);
@@ -325,8 +356,74 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
 
+  // T: wave tv = wave < 6 transforms column tv of every (tile, channel half) patch: lane (tile, h)
+  // forms e[r] = B_tv(d[r][.]) over the 6 patch rows (the row's taps: up to 4 columns with
+  // wave-uniform coefficients), then V[u][tv] = B_u(e) for u = 0..5, split into the operand chain
+  // and written to the V buffer at (6u + tv, h, tile) = the M phase's read address.
+  // waves 6 and 7 repeat columns 4 and 5 (the same values to the same addresses): every wave runs
+  // one code path, so the transform VALU can sit in the MFMA gaps of the same basic block
+  const int tv = wave < 6 ? wave : wave - 2;
+  int tcol[4];
+  float tk[4];
+  switch (tv) {
+    case 0: tcol[0] = 0; tcol[1] = 2; tcol[2] = 4; tcol[3] = 4; tk[0] = 4.f; tk[1] = -5.f; tk[2] = 1.f; tk[3] = 0.f; break;
+    case 1: tcol[0] = 1; tcol[1] = 2; tcol[2] = 3; tcol[3] = 4; tk[0] = -4.f; tk[1] = -4.f; tk[2] = 1.f; tk[3] = 1.f; break;
+    case 2: tcol[0] = 1; tcol[1] = 2; tcol[2] = 3; tcol[3] = 4; tk[0] = 4.f; tk[1] = -4.f; tk[2] = -1.f; tk[3] = 1.f; break;
+    case 3: tcol[0] = 1; tcol[1] = 2; tcol[2] = 3; tcol[3] = 4; tk[0] = -2.f; tk[1] = -1.f; tk[2] = 2.f; tk[3] = 1.f; break;
+    case 4: tcol[0] = 1; tcol[1] = 2; tcol[2] = 3; tcol[3] = 4; tk[0] = 2.f; tk[1] = -1.f; tk[2] = -2.f; tk[3] = 1.f; break;
+    default: tcol[0] = 1; tcol[1] = 3; tcol[2] = 5; tcol[3] = 5; tk[0] = 4.f; tk[1] = -5.f; tk[2] = 1.f; tk[3] = 0.f; break;
+  }
+  const int ttile = lane & 31, th = lane >> 5;
+  const int pbase = (4 * (ttile >> 4)) * kRS + 9 * (ttile & 15) + th;  // patch origin slot
+  const char* tb[4];       // this chunk's tap columns in the ring slot the transform reads
+  char* twm = nullptr;     // this lane's V entry of component tv (plane MH)
+  char* twl = nullptr;     // (plane L)
+  f32x4 td[4];             // the taps of the patch row being transformed next
+  f32x4 te[6];             // e[r]
+  auto t_begin = [&](int ck) {  // transform of chunk ck: addresses, and patch row 0's reads
+    const int p = ck & 1;
+    const char* rb = smem + kOffR + p * (kRingF * 4) + 16 * pbase;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) tb[t] = rb + 16 * (2 * tcol[t] + (tcol[t] >> 2));
+    twm = smem + p * (kVMH * 4) + tv * 1024 + 16 * lane;
+    twl = smem + kOffL + p * (kVL * 4) + tv * 512 + 8 * lane;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) td[t] = *reinterpret_cast<const f32x4*>(tb[t]);
+  };
+  // step s < 6: e[s] from row s's taps, then row s + 1's reads; step 6 + u: output u
+  auto t_step = [&](int s) {
+    if (s < 6) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        te[s][e] = __builtin_fmaf(tk[3], td[3][e], __builtin_fmaf(tk[2], td[2][e], __builtin_fmaf(tk[1], td[1][e], tk[0] * td[0][e])));
+      if (s < 5) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) td[t] = *reinterpret_cast<const f32x4*>(tb[t] + (s + 1) * kRS * 16);
+      }
+      return;
+    }
+    const int u = s - 6;
+    f32x4 x;
+    switch (u) {
+      case 0: x = bt_row<0>(te); break;
+      case 1: x = bt_row<1>(te); break;
+      case 2: x = bt_row<2>(te); break;
+      case 3: x = bt_row<3>(te); break;
+      case 4: x = bt_row<4>(te); break;
+      default: x = bt_row<5>(te); break;
+    }
+    const u32x6 ch = split3(x);
+    *reinterpret_cast<u32x4*>(twm + 6 * u * 1024) = u32x4{ch[0], ch[1], ch[2], ch[3]};
+    *reinterpret_cast<u32x2*>(twl + 6 * u * 512) = u32x2{ch[4], ch[5]};
+  };
+  // which transform steps run after component k's MFMAs (the VALU work beside the matrix pipe)
+  constexpr int kStep0[10] = {0, 1, 2, 3, 4, 5, 7, 9, 11, 12};  // steps kStep0[k] .. kStep0[k + 1] - 1
+
   auto comp_of = [&](int k) { return 6 * (cu0 + k / 3) + cv0 + k % 3; };
-  auto do_mfma = [&](int ck) {
+  // one chunk: M(ck) on V[ck & 1], interleaved with T(ck + 1) into V[(ck + 1) & 1]; the raw input
+  // of chunk ck + 2 goes into the ring slot T(ck) has read
+  auto do_chunk = [&](int ck) {
+    constexpr bool tr = KRRN_W4_EXP != 3;
     const int p = ck & 1;
     const char* vm = smem + p * (kVMH * 4) + 16 * lane;
     const char* vlo = smem + kOffL + p * (kVL * 4) + 8 * lane;
@@ -337,7 +434,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     };
     f32x4 raw[3];
     const bool stage = ck + 2 < nck && KRRN_W4_EXP != 4;
-    if (stage) load_raw(ck + 2, raw);
+    if (tr) t_begin(ck + 1 < nck ? ck + 1 : ck + 1 - 2);  // past the last chunk: a harmless repeat
     u32x6 acn = chain(0);
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
@@ -356,9 +453,28 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 #if KRRN_W4_EXP != 2
       if (k < 6) load_w(ck, k + 3); else load_w(ck + 1, k - 6);
 #endif
-      __builtin_amdgcn_sched_barrier(0);  // keep the reload here (hipcc otherwise sinks it below the MFMAs)
+      if constexpr (tr) {
+#pragma unroll
+        for (int st = kStep0[k]; st < kStep0[k + 1]; ++st) t_step(st);
+      }
+      // the raw input of chunk ck + 2: loaded here (3 components before its store) rather than at
+      // the chunk's start, so its 12 registers are not live beside the transform's row steps
+      if (k == KRRN_W4_RAWK && stage) load_raw(ck + 2, raw);
+      // issue shape of the slot: the next operands' LDS reads first, then the three MFMAs with the
+      // transform VALU in their gaps (one wave's in-order issue would otherwise wait out each
+      // dependent MFMA), then the weight reload
+#if KRRN_W4_GAP > 0
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // DS reads
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, KRRN_W4_GAP, 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, KRRN_W4_GAP, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, KRRN_W4_GAP, 0);
+#endif
+      __builtin_amdgcn_sched_barrier(0);  // keep each component's reload and transform steps in place
     }
-    if (stage) store_raw(p, raw);  // chunk ck + 2 into the slot chunk ck's transform has read
+    if (stage) store_raw(p, raw);
   };
 
   // prologue: raw chunks 0 and 1 to the ring, T(0), weights of chunk 0
@@ -374,12 +490,15 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 #pragma unroll
   for (int k = 0; k < 3; ++k) load_w(0, k);
   __syncthreads();
-  do_transform(0);
+  if (KRRN_W4_EXP != 3) {
+    t_begin(0);
+#pragma unroll
+    for (int st = 0; st < 12; ++st) t_step(st);
+  }
   __syncthreads();
 
   for (int ck = 0; ck < nck; ++ck) {
-    do_mfma(ck);
-    do_transform(ck + 1);
+    do_chunk(ck);
     // LDS-only hand-offs (ring and V buffers): lgkmcnt, not the in-flight weight loads
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
@@ -393,31 +512,34 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     return;
   }
 #endif
-  // epilogue: 2 passes of 16 tiles (accumulator rows 8 pass .. 8 pass + 7 of each lane: tiles
-  // 16 pass + (r & 3) + 8 ((r >> 2) & 1) + 4 h); a pass's stores free its 72 accumulator registers
-  const int en = tid & 63, ei = (tid >> 6) & 3, etq = 2 * (tid >> 8);  // ei, etq wave-uniform
-  const int ng = n0 + en;
+  // epilogue: 2 passes of 16 tiles (accumulator rows 8 pass .. 8 pass + 7 of each lane: local tile
+  // (r & 3) + 8 ((r >> 2) & 1) + 4 h of the pass); a pass's stores free its 72 accumulator registers.
+  // Then wave w forms output row i = w & 3 of tile groups (w >> 2) and (w >> 2) + 2: lane (tile of
+  // the group, channel quad) -> float4 channel-run stores.
+  const int enq = lane & 15, etl = lane >> 4, ei = wave & 3;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    char* ew = smem + (32 * nh + fr) * 16;
+    char* ew = smem + (32 * nh + fr) * 4;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const int comp = comp_of(k);
 #pragma unroll
-      for (int hq = 0; hq < 2; ++hq) {
-        const int r0 = 8 * pass + 4 * hq;
-        const f32x4 v4 = {acc[k][r0], acc[k][r0 + 1], acc[k][r0 + 2], acc[k][r0 + 3]};
-        *reinterpret_cast<f32x4*>(ew + (comp * 4 + 2 * hq + h) * kEQ) = v4;
+      for (int q = 0; q < 8; ++q) {
+        const int r = 8 * pass + q;
+        const int tl = (r & 3) + 8 * ((r >> 2) & 1) + 4 * h;
+        *reinterpret_cast<float*>(ew + (comp * 16 + tl) * kET) = acc[k][r];
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
+    for (int it = 0; it < 2; ++it) {
+      const int tl = 4 * ((wave >> 2) + 2 * it) + etl;
+      const int ng = n0 + 4 * enq;
       switch (ei) {
-        case 0: epi_row<0>(a, smem, en, etq + qq, pass, b, ty0, tx0, ng); break;
-        case 1: epi_row<1>(a, smem, en, etq + qq, pass, b, ty0, tx0, ng); break;
-        case 2: epi_row<2>(a, smem, en, etq + qq, pass, b, ty0, tx0, ng); break;
-        default: epi_row<3>(a, smem, en, etq + qq, pass, b, ty0, tx0, ng); break;
+        case 0: epi_row<0, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
+        case 1: epi_row<1, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
+        case 2: epi_row<2, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
+        default: epi_row<3, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
       }
     }
     __syncthreads();
@@ -442,11 +564,52 @@ KRRN_API int krrn_conv3x3_wino4_x3_f32(const float* in, int in_cs, int in_co, in
   a.res = res; a.res_cs = res_cs; a.res_co = res_co;
   a.out = out; a.out_cs = out_cs; a.out_co = out_co; a.relu = relu;
   a.Ht = (H + 3) / 4; a.Wt = (W + 3) / 4;
+  const bool ov = !(out_cs & 3) && !(out_co & 3) && krrn_aligned16(out);
+  const bool rv = !res || (!(res_cs & 3) && !(res_co & 3) && krrn_aligned16(res));
+  const bool sv = (!scale || krrn_aligned16(scale)) && (!bias || krrn_aligned16(bias));
+  a.vec = (ov && rv && sv) ? 1 : 0;
+  a.w1 = nullptr; a.part = nullptr;
   // 32-bit buffer offsets: one image, and the MH plane (records x 16 B)
   const long long nrec = (long long)(cin / kC) * 36 * N * 2;
   if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kN);
   if (rb > 0x7fffffffLL) return KRRN_ESHAPE;
-  hipLaunchKernelGGL(wino_f43_x3_kernel, dim3((unsigned)rb), dim3(512), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(wino_f43_x3_kernel<false>, dim3((unsigned)rb), dim3(512), 0, (hipStream_t)stream, a);
+  return krrn_launch_status();
+}
+
+KRRN_API int krrn_conv3x3_wino4_x3_head_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
+                                            const void* U3, int N, const float* scale, const float* bias,
+                                            const float* res, int res_cs, int res_co, int relu, const float* w1,
+                                            const float* b1, int p1, float* part, float* out, int out_c,
+                                            void* stream) {
+  if (!in || !U3 || !w1 || !part || !out) return KRRN_EARG;
+  if (B < 1 || H < 1 || W < 1 || N < 4 || (N & 3) || p1 < 1 || p1 > 4 || out_c < p1) return KRRN_ESHAPE;
+  if (cin < kC || (cin % kC) || in_co + cin > in_cs) return KRRN_EALIGN;
+  if (!krrn_aligned16(U3) || (((uintptr_t)in) & 15u) || (in_cs & 3) || (in_co & 3)) return KRRN_EALIGN;
+  if (!krrn_aligned16(w1) || !krrn_aligned16(part)) return KRRN_EALIGN;
+  if ((scale && !krrn_aligned16(scale)) || (bias && !krrn_aligned16(bias))) return KRRN_EALIGN;
+  if (res && ((res_cs & 3) || (res_co & 3) || !krrn_aligned16(res))) return KRRN_EALIGN;
+  Wino4Args a;
+  a.in = in; a.in_cs = in_cs; a.in_co = in_co; a.B = B; a.H = H; a.W = W; a.cin = cin;
+  a.img = (long long)H * W * in_cs;
+  a.U3 = U3; a.N = N; a.n_store = N; a.scale = scale; a.bias = bias;
+  a.res = res; a.res_cs = res_cs; a.res_co = res_co;
+  a.out = nullptr; a.out_cs = 0; a.out_co = 0; a.relu = relu; a.vec = 1;
+  a.Ht = (H + 3) / 4; a.Wt = (W + 3) / 4;
+  a.w1 = w1; a.part = part;
+  const long long nrec = (long long)(cin / kC) * 36 * N * 2;
+  if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
+  const int nbn = krrn_cdiv(N, kN);
+  const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * nbn;
+  const long long M = (long long)B * H * W;
+  const long long fb = (M + 255) / 256;
+  if (rb > 0x7fffffffLL || fb > 0x7fffffffLL) return KRRN_ESHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wino_f43_x3_kernel<true>, dim3((unsigned)rb), dim3(512), 0, s, a);
+  const int st = krrn_launch_status();
+  if (st != KRRN_OK) return st;
+  hipLaunchKernelGGL(wino4_head_finish_kernel, dim3((unsigned)fb), dim3(256), 0, s, part, nbn, M, H * W, b1, p1, out,
+                     out_c);
   return krrn_launch_status();
 }

@@ -28,10 +28,9 @@ import torch.nn as nn
 from . import knobs, ops
 from .config import load_hrnet_spec
 from .ops import Act, pad4
-from .runtime import add_conv_group, add_gemm, add_small_group, Plan, add_conv, ptr
+from .runtime import add_conv_group, add_gemm, Plan, add_conv, ptr
 
 # switches (pose_estimation_amd/knobs.py has each one's meaning)
-HR_GROUP = knobs.flag("KRRN_HR_GROUP")
 DECONV_FOLD = knobs.flag("KRRN_DECONV_FOLD")
 CONVT_GROUP = knobs.flag("KRRN_CONVT_GROUP")
 SMALL_CONV = knobs.flag("KRRN_SMALL_CONV")
@@ -42,6 +41,9 @@ WINO_X3 = knobs.flag("KRRN_WINO_X3")
 # Winograd of the conv before it (krrn_conv3x3_wino_x3_head_f32): its 128-channel input map is never
 # written or re-read
 HEAD_FUSE = knobs.flag("KRRN_HEAD_FUSE")
+# each HRNet fuse output waits for the branches it reads through capture edges (runtime.Edge)
+# instead of the module barrier (join into stream 0 + fork)
+FUSE_EDGES = knobs.flag("KRRN_FUSE_EDGES")
 # the fuse-layer work that reads only branch j's output (the 1x1 convs of the j > i terms, all but
 # the last stride-2 conv of the j < i chains) runs on branch j's stream right after its blocks,
 # beside the other branches' tails, instead of after the join on the output's stream
@@ -268,7 +270,8 @@ class _Builder:
         if not ops.wino_eligible(spec, M) or (Ho, Wo) != (x.H, x.W):
             return False
         np_ = pad4(spec.cout)
-        U = ops.wino_weights_x3(ops.wino_weights(conv, self.dev, cin_p=x.cp))
+        f4 = ops.wino4_eligible(spec, x, Ho, Wo)
+        U = ops.wino_weights_x3((ops.wino4_weights if f4 else ops.wino_weights)(conv, self.dev, cin_p=x.cp))
         w1 = torch.zeros(4, np_, device=self.dev)
         w1[:final.out_channels, :spec.cout] = final.weight.detach().reshape(final.out_channels, -1).float().to(self.dev)
         b1 = None
@@ -277,12 +280,15 @@ class _Builder:
             b1[:final.out_channels] = final.bias.detach().float().to(self.dev)
         self.specs += [spec, U, w1] + ([b1] if b1 is not None else [])
         part = self.plan.scratch(((np_ + 63) // 64) * M * 4)
-        tiles = x.B * ((Ho + 1) // 2) * ((Wo + 1) // 2)
-        pipe = 2.0 * 16 * spec.cin_p * np_ * tiles
-        meta = dict(kernel="wino_f23_x3_head", tag="conv_wino_head", M=M, N=np_, K=spec.cin_p * 9,
-                    flops=2.0 * spec.cin * spec.cout * 9 * M + 2.0 * spec.cout * n_store * M,
+        if f4:
+            pipe = 2.0 * 36 * spec.cin_p * np_ * x.B * ((Ho + 3) // 4) * ((Wo + 3) // 4)
+        else:
+            pipe = 2.0 * 16 * spec.cin_p * np_ * x.B * ((Ho + 1) // 2) * ((Wo + 1) // 2)
+        meta = dict(kernel="wino_f43_x3_head" if f4 else "wino_f23_x3_head", tag="conv_wino_head", M=M, N=np_,
+                    K=spec.cin_p * 9, flops=2.0 * spec.cin * spec.cout * 9 * M + 2.0 * spec.cout * n_store * M,
                     mfma_flops=pipe * 6 / 16, mfma_bf16_flops=pipe * 6)
-        self.plan.add("krrn_conv3x3_wino_x3_head_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, ptr(U), np_,
+        self.plan.add("krrn_conv3x3_wino4_x3_head_f32" if f4 else "krrn_conv3x3_wino_x3_head_f32", ptr(x.t), x.cs,
+                      x.co, x.B, x.H, x.W, spec.cin_p, ptr(U), np_,
                       ptr(spec.scale), ptr(spec.bias), ptr(None), 0, 0, 1, ptr(w1), ptr(b1), n_store, ptr(part),
                       ptr(out), out.shape[1], meta=meta)
         return True
@@ -414,40 +420,6 @@ class _Builder:
                      out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=osy, osx=osx, ooy=ooy,
                      oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag, wt3=ptr(w3) if w3 is not None else None)
 
-    def small_grouped(self, xs: List[Act], convs: List[Tuple[nn.Module, nn.Module]], res: Optional[List[Act]],
-                      tag: str) -> Optional[List[Act]]:
-        """The i-th conv on xs[i] for every branch as ONE krrn_conv_small_group_f32 launch, or
-        None (nothing emitted) when one of them is not a small-conv problem."""
-        specs = []
-        for x, (conv, bn) in zip(xs, convs):
-            spec = ops.make_conv(conv, bn, self.dev, cin_p=x.cp)
-            if not ops.small_conv_eligible(spec, x):
-                return None
-            specs.append(spec)
-        self.specs.extend(specs)
-        outs = [self.act(x.H, x.W, spec.cout) for x, spec in zip(xs, specs)]
-        probs = [self.small_problem(x, spec, o, res[i] if res is not None else None, True)
-                 for i, (x, spec, o) in enumerate(zip(xs, specs, outs))]
-        add_small_group(self.plan, probs, tag=tag)
-        return outs
-
-    def branches_grouped(self, xs: List[Act], m: "HighResolutionModule") -> Optional[List[Act]]:
-        """All branches of a module, block by block: the j-th conv of every branch in ONE grouped
-        small-conv launch (myhrnet.py:226-231 runs branch i's BasicBlocks on x[i]; nothing couples
-        them). None (nothing emitted) when a branch conv is not a small-conv problem: every depth
-        has the first one's shapes, so that is decided before anything is emitted."""
-        cur = list(xs)
-        for bi in range(len(m.branches[0])):
-            blks = [m.branches[i][bi] for i in range(m.num_branches)]
-            hs = self.small_grouped(cur, [(b.conv1, b.bn1) for b in blks], None, "hr_branch_conv1")
-            if hs is None:
-                assert bi == 0
-                return None
-            ys = self.small_grouped(hs, [(b.conv2, b.bn2) for b in blks], cur, "hr_branch_conv2")
-            assert ys is not None  # conv2 has conv1's output shape and width
-            cur = ys
-        return cur
-
     def resize(self, x: Act, out: Act, add: Optional[Act] = None, align: bool = False, relu: bool = False):
         assert x.cp == out.cp
         self.plan.add("krrn_resize_bilinear_f32", ptr(x.t), x.B, x.H, x.W, x.cs, x.co, x.cp, ptr(out.t), out.H,
@@ -481,28 +453,32 @@ class _Builder:
         plan = self.plan
         nb = m.num_branches
         side = list(range(1, nb))
-        groupable = HR_GROUP and SMALL_CONV and 1 < nb <= 4 and all(
-            len(m.branches[i]) == len(m.branches[0]) for i in range(nb)) and all(
-            isinstance(b, BasicBlock) and b.downsample is None for br in m.branches for b in br)
-        ys = self.branches_grouped(xs, m) if groupable else None
         pre = {}
-        if ys is None:
-            ys = []
-            if fork_in:
-                plan.fork(side)
-            for i, x in enumerate(xs):
-                with plan.on_stream(i):
-                    y = x
-                    for blk in m.branches[i]:
-                        y = self.basic(y, blk)
-                    if nb > 1 and FUSE_EARLY:
-                        pre.update(self._fuse_terms_from(y, m, i))
-                ys.append(y)
+        ys = []
+        if fork_in:
+            plan.fork(side)
+        for i, x in enumerate(xs):
+            with plan.on_stream(i):
+                y = x
+                for blk in m.branches[i]:
+                    y = self.basic(y, blk)
+                if nb > 1 and FUSE_EARLY:
+                    pre.update(self._fuse_terms_from(y, m, i))
+            ys.append(y)
+        if not FUSE_EDGES or nb == 1:
             plan.join(side)
         if nb == 1:
             return ys
         fused = []
-        plan.fork(side)
+        if FUSE_EDGES:
+            # fuse output i (stream i) waits for exactly the branches it reads (all of them, each
+            # with its early terms), not for a join of every branch into stream 0 and a fork back
+            for i in range(nb):
+                for j in range(nb):
+                    if j != i:
+                        plan.edge(j, i)
+        else:
+            plan.fork(side)
         for i in range(nb):
             with plan.on_stream(i):
                 fused.append(self._fuse_output(ys, m, i, outs[i] if outs is not None else None, pre))
@@ -584,7 +560,7 @@ def build_hrnet_plan(net: HRNet, plan: Plan, x: Act, after_layer1=None) -> Tuple
         nb = net.stage_branches[si]
         # per-stream stages: every module of the stage chains per stream (the grouped form runs on
         # stream 0, so not with it)
-        cross = STAGE_STREAMS and MODULE_STREAMS and not HR_GROUP and all(m.num_branches > 1 for m in stage)
+        cross = STAGE_STREAMS and MODULE_STREAMS and all(m.num_branches > 1 for m in stage)
         if on_streams and not cross:
             # the previous stage left branch k on stream k, but this stage runs its transitions on
             # stream 0 and forks from it: join first (not reached with W18 / W32 / W48, where every
@@ -619,7 +595,7 @@ def build_hrnet_plan(net: HRNet, plan: Plan, x: Act, after_layer1=None) -> Tuple
                 xl.append(src)
         last_stage = si == nstages - 1
         for mi, m in enumerate(stage):
-            chain = MODULE_STREAMS and m.num_branches > 1 and not HR_GROUP  # the grouped form runs on stream 0
+            chain = MODULE_STREAMS and m.num_branches > 1
             fork_in = not chain or (mi == 0 and not cross)
             join_out = not chain or (mi == len(stage) - 1 and (last_stage or not cross))
             xl = bld.hr_module(xl, m, fork_in=fork_in, join_out=join_out)

@@ -33,10 +33,9 @@ KNOBS: Dict[str, Tuple[Optional[str], str]] = {
     "KRRN_MODULE_STREAMS": ("1", "consecutive HRNet modules of a stage keep each branch on its stream (no barrier between them)"),
     "KRRN_STAGE_STREAMS": ("1", "with KRRN_MODULE_STREAMS, HRNet stages chain per branch stream too (transitions on their branch's stream)"),
     "KRRN_FUSION_EARLY": ("1", "the fusion work that reads only the input cloud runs beside the HRNet phase (side stream)"),
+    "KRRN_FUSE_EDGES": ("1", "each HRNet fuse output waits for exactly its branches (capture edges); 0 = module barrier"),
     "KRRN_HEAD_FUSE": ("1", "a <= 4-output final 1x1 fused into the head's last split Winograd; 0 = two launches"),
     "KRRN_SMALL_CONV": ("1", "HRNet branch / fuse convs on the LDS-slab conv_small kernel; 0 = implicit GEMM"),
-    "KRRN_HR_GROUP": ("0", "the four branches' j-th convs as one grouped conv_small launch (measured "
-                           "slower in the step); 0 = per-branch chains on plan streams"),
     "KRRN_GEMM_1X1": ("1", "stride-1 1x1 convs as plain GEMMs; 0 = implicit-GEMM conv"),
     "KRRN_CONVT_GROUP": ("1", "the transposed conv's four phase convs as one grouped launch; 0 = four"),
     "KRRN_DECONV_FOLD": ("1", "fold last_layer_2 into the deconv (272 instead of 400 input channels); "

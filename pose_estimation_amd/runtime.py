@@ -50,10 +50,10 @@ _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I
 _lib.register("krrn_conv3x3_wino_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv3x3_wino4_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv3x3_wino_x3_head_f32", [P, I, I, I, I, I, I, P, I, P, P, P, I, I, I, P, P, I, P, P, I, P])
+_lib.register("krrn_conv3x3_wino4_x3_head_f32", [P, I, I, I, I, I, I, P, I, P, P, P, I, I, I, P, P, I, P, P, I, P])
 _lib.register("krrn_conv1x1_nchw_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
 _lib.register("krrn_conv1x1_nchw_x3_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])
 _lib.register("krrn_conv_small_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, I, I, I, I, P])
-_lib.register("krrn_conv_small_group_f32", [P, I, P])
 _lib.register("krrn_blas_gemm_create", [I, I, I, I, I, I, L, L, I, I, I, I, L, L, P, P])
 _lib.register("krrn_blas_gemm_run", [P, P, P, P, P, P, P, L, P])
 _lib.register("krrn_blas_gemm_destroy", [P])
@@ -145,6 +145,57 @@ class Sync:
         streams[self.dst].wait_event(self.event)
 
 
+class _CaptureDeps:
+    """hipStreamGetCaptureInfo_v2 + hipStreamUpdateCaptureDependencies (the HIP runtime torch uses):
+    make a capturing stream depend on another capturing stream's current leaf nodes without an
+    event. Side-stream-to-side-stream event waits made hipGraph capture segfault at capture end on
+    this image whenever several of them crossed (profiles/hip_capture_crosswait.py, rc 139 with the
+    events kept alive or not); the same dependencies as capture edges replay correctly
+    (profiles/hip_capture_deps.py, round 6)."""
+    _hip = None
+
+    @classmethod
+    def hip(cls):
+        if cls._hip is None:
+            h = ctypes.CDLL("libamdhip64.so")
+            h.hipStreamGetCaptureInfo_v2.argtypes = [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulonglong),
+                                                     ctypes.POINTER(P), ctypes.POINTER(ctypes.POINTER(P)),
+                                                     ctypes.POINTER(ctypes.c_size_t)]
+            h.hipStreamUpdateCaptureDependencies.argtypes = [P, ctypes.POINTER(P), ctypes.c_size_t, ctypes.c_uint]
+            cls._hip = h
+        return cls._hip
+
+    @classmethod
+    def add(cls, src: "torch.cuda.Stream", dst: "torch.cuda.Stream") -> bool:
+        """dst's next captured work depends on everything captured on src so far; False (nothing
+        done) when src is not capturing."""
+        h = cls.hip()
+        st, cid, graph = ctypes.c_int(), ctypes.c_ulonglong(), P()
+        deps, n = ctypes.POINTER(P)(), ctypes.c_size_t()
+        e = h.hipStreamGetCaptureInfo_v2(P(src.cuda_stream), ctypes.byref(st), ctypes.byref(cid), ctypes.byref(graph),
+                                         ctypes.byref(deps), ctypes.byref(n))
+        if e != 0 or st.value != 1:  # hipStreamCaptureStatusActive
+            return False
+        nodes = (P * max(1, n.value))(*[deps[k] for k in range(n.value)])
+        e = h.hipStreamUpdateCaptureDependencies(P(dst.cuda_stream), nodes, n.value, 0)  # hipStreamAddCaptureDependencies
+        if e != 0:
+            raise RuntimeError(f"hipStreamUpdateCaptureDependencies failed ({e})")
+        return True
+
+
+class Edge(Sync):
+    """Sync between two side streams: a capture edge (_CaptureDeps) under hipGraph capture, an
+    event record / wait otherwise."""
+    __slots__ = ()
+
+    def __call__(self, env: Dict[str, Any]):
+        streams = env["__streams__"]
+        if streams is None:  # serial run
+            return
+        if not _CaptureDeps.add(streams[self.src], streams[self.dst]):
+            Sync.__call__(self, env)
+
+
 # KRRN_DIAG_DROP=name[,name...]: leave every launch of those C-ABI entry points out of new plans.
 # A what-if timing diagnostic (profiles/whatif.sh: how much the step shrinks if a kernel family
 # were free); the outputs are meaningless with it set, and nothing in the package sets it.
@@ -232,6 +283,13 @@ class Plan:
         if src != dst:
             self.nstreams = max(self.nstreams, src + 1, dst + 1)
             self.ops.append(Sync(src, dst))
+
+    def edge(self, src: int, dst: int):
+        """Stream `dst` waits for all work so far on stream `src`, as a capture edge (Edge): for
+        dependencies between two side streams."""
+        if src != dst:
+            self.nstreams = max(self.nstreams, src + 1, dst + 1)
+            self.ops.append(Edge(src, dst))
 
     def side_streams(self) -> List[torch.cuda.Stream]:
         while len(self._side) < self.nstreams - 1:
@@ -367,33 +425,6 @@ def add_conv(plan: Plan, *, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps,
 
 
 GROUP_TILE = 6
-
-
-class SmallDesc(ctypes.Structure):
-    """krrn_small_desc (include/krrn_hip.h): the arguments of krrn_conv_small_f32."""
-    _fields_ = [("in_", P), ("in_cs", I), ("in_co", I), ("B", I), ("H", I), ("W", I), ("cin", I), ("wt", P), ("N", I),
-                ("n_store", I), ("scale", P), ("bias", P), ("res", P), ("res_cs", I), ("res_co", I), ("out", P),
-                ("out_cs", I), ("out_co", I), ("relu", I), ("ksize", I), ("stride", I), ("nw", I), ("ks", I)]
-
-
-def add_small_group(plan: Plan, problems: List[dict], tag: str = "small_group"):
-    """One krrn_conv_small_group_f32 launch over up to 4 independent small convs (dicts of
-    SmallDesc fields, `in_` as `x`, plus 'flops' / 'mfma_flops' for the breakdown)."""
-    n = len(problems)
-    arr = (SmallDesc * n)()
-    flops = mfma = 0.0
-    shapes = []
-    for q, pr in enumerate(problems):
-        pr = dict(pr)
-        flops += pr.pop("flops")
-        mfma += pr.pop("mfma_flops")
-        pr["in_"] = pr.pop("x")
-        arr[q] = SmallDesc(**pr)
-        shapes.append((pr.pop("M"), pr["N"], pr["ksize"] ** 2 * pr["cin"], 1))
-    plan.buffers.append(arr)
-    plan.add("krrn_conv_small_group_f32", ctypes.cast(arr, P), n,
-             meta=dict(kernel="conv_small_group", flops=flops, tag=tag, M=shapes[0][0], N=shapes[0][1],
-                       K=shapes[0][2], splits=1, shapes=shapes, mfma_flops=mfma))
 
 
 def conv_desc(*, x, x_cs, x_co, B, Hi, Wi, cin_p, Hg, Wg, in_s, taps, wt, N, n_store, scale, bias, res=None,

@@ -15,7 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pose_estimation_amd import KRRN, make_config  # noqa: E402
 from pose_estimation_amd.pipeline import BatchPipeline, PipelinedPipeline  # noqa: E402
-from pose_estimation_amd.runtime import ConvDesc, Op, SmallDesc  # noqa: E402
+from pose_estimation_amd.runtime import ConvDesc, Op  # noqa: E402
 from pose_estimation_amd.synthetic import init_weights, make_batch  # noqa: E402
 
 dev = torch.device("cuda", 0)
@@ -80,8 +80,8 @@ def pointers(op):
             for k, v in enumerate(a):
                 if isinstance(v, int) and v > (1 << 40):
                     out.append((f"{ai}[{k}]", v))
-    if op.name in ("krrn_conv2d_group_x3_f32", "krrn_conv2d_group_f32", "krrn_conv_small_group_f32"):
-        st = SmallDesc if op.name == "krrn_conv_small_group_f32" else ConvDesc
+    if op.name in ("krrn_conv2d_group_x3_f32", "krrn_conv2d_group_f32"):
+        st = ConvDesc
         n = op.args[1]
         descs = ctypes.cast(ctypes.c_void_p(op.args[0].value), ctypes.POINTER(st * n)).contents
         for q in range(n):

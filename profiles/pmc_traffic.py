@@ -21,6 +21,10 @@ def _short(name: str) -> str:
     m = re.search(r"conv_group_kernel<(\d+), (\d+), (\d+), \d+>", name)
     if m:
         return f"conv_group<{m.group(1)},{m.group(2)},{m.group(3)}>"
+    if "wino_f43_x3_kernel<true>" in name:
+        return "wino_f43_x3_head"
+    if "wino_f43_x3" in name:
+        return "wino_f43_x3"
     if "wino_f23_x3_kernel<true>" in name:
         return "wino_f23_x3_head"
     if "wino_f23_x3" in name:

@@ -390,13 +390,15 @@ def test_conv3x3_winograd4(dev, cin, cout, H, W, co, relu):
     assert torch.all(t[..., :co] == 7.0) and torch.all(t[..., co + np_:] == 7.0)
 
 
-@pytest.mark.parametrize("cin,cout,H,W,co,p1,with_res", [
-    (128, 128, 120, 120, 0, 3, False), (64, 72, 17, 23, 4, 4, True), (20, 132, 9, 8, 0, 1, True),
-    (36, 40, 7, 9, 8, 2, False)])
-def test_conv3x3_winograd_head(dev, cin, cout, H, W, co, p1, with_res):
-    """krrn_conv3x3_wino_x3_head_f32: the last head conv (+ BN, residual, ReLU) and a <= 4-output
-    1x1 + bias in one launch (NML's 120-px conv + nml_final at B = 3, ragged 64-channel blocks, odd
-    maps) vs torch fp32; the NCHW channels past p1 are not written."""
+@pytest.mark.parametrize("cin,cout,H,W,co,p1,with_res,f4", [
+    (128, 128, 120, 120, 0, 3, False, False), (64, 72, 17, 23, 4, 4, True, False), (20, 132, 9, 8, 0, 1, True, False),
+    (36, 40, 7, 9, 8, 2, False, False), (128, 128, 120, 120, 0, 3, False, True), (64, 72, 33, 37, 4, 4, True, True),
+    (96, 132, 40, 35, 8, 1, True, True)])
+def test_conv3x3_winograd_head(dev, cin, cout, H, W, co, p1, with_res, f4):
+    """krrn_conv3x3_wino_x3_head_f32 / krrn_conv3x3_wino4_x3_head_f32 (f4): the last head conv (+ BN,
+    residual, ReLU) and a <= 4-output 1x1 + bias in one launch (NML's 120-px conv + nml_final at B = 3,
+    ragged 64-channel blocks and tiles, odd maps) vs torch fp32; the NCHW channels past p1 are not
+    written."""
     from pose_estimation_amd import _lib
     from pose_estimation_amd.runtime import P, ptr
     g = torch.Generator().manual_seed(cin + 3 * cout + H + p1)
@@ -414,7 +416,7 @@ def test_conv3x3_winograd_head(dev, cin, cout, H, W, co, p1, with_res):
     ref = final(torch.relu(h + res if with_res else h)).detach()
     xa = _nhwc(x, dev, cs=ops.pad4(cin) + co + 4, co=co)
     spec = ops.make_conv(conv, bn, dev, cin_p=ops.pad4(cin))
-    U3 = ops.wino_weights_x3(ops.wino_weights(conv, dev, cin_p=ops.pad4(cin)))
+    U3 = ops.wino_weights_x3((ops.wino4_weights if f4 else ops.wino_weights)(conv, dev, cin_p=ops.pad4(cin)))
     np_ = ops.pad4(cout)
     w1 = torch.zeros(4, np_, device=dev)
     w1[:p1, :cout] = final.weight.detach().reshape(p1, cout).to(dev)
@@ -423,7 +425,8 @@ def test_conv3x3_winograd_head(dev, cin, cout, H, W, co, p1, with_res):
     part = torch.full((((np_ + 63) // 64) * B * H * W * 4,), float("nan"), device=dev)
     out = torch.full((B, p1 + 1, H, W), -7.0, device=dev)
     L = _lib.lib()
-    _lib.check(L.krrn_conv3x3_wino_x3_head_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_,
+    fn = L.krrn_conv3x3_wino4_x3_head_f32 if f4 else L.krrn_conv3x3_wino_x3_head_f32
+    _lib.check(fn(ptr(xa.t), xa.cs, xa.co, B, H, W, ops.pad4(cin), ptr(U3), np_,
                                                ptr(spec.scale), ptr(spec.bias), ptr(ra.t) if ra else ptr(None),
                                                ra.cs if ra else 0, 0, 1, ptr(w1), ptr(b1), p1, ptr(part), ptr(out),
                                                p1 + 1, P(torch.cuda.current_stream().cuda_stream)), "wino_head")

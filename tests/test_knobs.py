@@ -58,7 +58,7 @@ def test_undeclared_knob_is_an_error():
 def test_defaults_are_the_shipped_configuration(monkeypatch):
     for k in knobs.KNOBS:
         monkeypatch.delenv(k, raising=False)
-    assert knobs.flag("KRRN_WINO_X3") and knobs.flag("KRRN_GRAPH") and not knobs.flag("KRRN_HR_GROUP")
+    assert knobs.flag("KRRN_WINO_X3") and knobs.flag("KRRN_GRAPH") and not knobs.flag("KRRN_DIAG_DROP")
     assert knobs.integer("KRRN_FUSION_CHUNK") == 16 and knobs.text("KRRN_HIP_LIB") is None
-    monkeypatch.setenv("KRRN_HR_GROUP", "1")
-    assert knobs.flag("KRRN_HR_GROUP")
+    monkeypatch.setenv("KRRN_FUSE_EDGES", "0")
+    assert not knobs.flag("KRRN_FUSE_EDGES")
