@@ -68,8 +68,14 @@ constexpr unsigned kOOB = 0xFFFF0000u;
 #ifndef KRRN_W4_EXP
 #define KRRN_W4_EXP 0
 #endif
+#ifndef KRRN_W4_DMA
+#define KRRN_W4_DMA 1  // raw staging by LDS-DMA (0: through registers)
+#endif
+#ifndef KRRN_W4_TDUP
+#define KRRN_W4_TDUP 0  // 1: waves 6, 7 repeat columns 4, 5 (one code path, 5 % slower); 0: they and the last chunk skip it
+#endif
 #ifndef KRRN_W4_RAWK
-#define KRRN_W4_RAWK 6  // component slot after which the next raw chunk is loaded
+#define KRRN_W4_RAWK 6  // component slot after which the next raw chunk is loaded (-1: chunk start)
 #endif
 #ifndef KRRN_W4_GAP
 #define KRRN_W4_GAP 6  // transform VALU instructions placed in each MFMA gap
@@ -308,7 +314,11 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   unsigned roff[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
+#if KRRN_W4_DMA
+    const int s = 192 * wave + 64 * i + lane;  // LDS-DMA: wave instruction i fills slots 64 (3 wave + i) ..
+#else
     const int s = tid + 512 * i;
+#endif
     const int r = s / kRS, q = s - (s / kRS) * kRS;
     const int g4 = q / 9, w9 = q - (q / 9) * 9;
     const int col = 4 * g4 + (w9 >> 1), hh = w9 & 1;
@@ -320,6 +330,15 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       raw[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, roff[i], ck * kC * 4, 0));
+  };
+  // raw chunk ck straight into ring slot `slot` by LDS-DMA (buffer_load_dwordx4 ... lds: 1 KB per
+  // wave instruction, no staging registers); padding slots receive zeros
+  auto dma_raw = [&](int ck, int slot) {
+    char* dst = smem + kOffR + slot * (kRingF * 4) + 3 * 1024 * wave;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(dst + 1024 * i), 16,
+                                               roff[i], ck * kC * 4, 0, 0);
   };
   auto store_raw = [&](int slot, const f32x4 (&raw)[3]) {
     char* dst = smem + kOffR + slot * (kRingF * 4) + 16 * tid;
@@ -423,7 +442,11 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   // one chunk: M(ck) on V[ck & 1], interleaved with T(ck + 1) into V[(ck + 1) & 1]; the raw input
   // of chunk ck + 2 goes into the ring slot T(ck) has read
   auto do_chunk = [&](int ck) {
+#if KRRN_W4_TDUP
     constexpr bool tr = KRRN_W4_EXP != 3;
+#else
+    const bool tr = KRRN_W4_EXP != 3 && wave < 6 && ck + 1 < nck;  // waves 6, 7 and the last chunk: no T
+#endif
     const int p = ck & 1;
     const char* vm = smem + p * (kVMH * 4) + 16 * lane;
     const char* vlo = smem + kOffL + p * (kVL * 4) + 8 * lane;
@@ -434,6 +457,10 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     };
     f32x4 raw[3];
     const bool stage = ck + 2 < nck && KRRN_W4_EXP != 4;
+#if KRRN_W4_DMA
+    if (KRRN_W4_RAWK < 0 && stage) dma_raw(ck + 2, p);  // into the slot T(ck) read during chunk ck - 1
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     if (tr) t_begin(ck + 1 < nck ? ck + 1 : ck + 1 - 2);  // past the last chunk: a harmless repeat
     u32x6 acn = chain(0);
 #pragma unroll
@@ -453,13 +480,16 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 #if KRRN_W4_EXP != 2
       if (k < 6) load_w(ck, k + 3); else load_w(ck + 1, k - 6);
 #endif
-      if constexpr (tr) {
+      if (tr) {
 #pragma unroll
         for (int st = kStep0[k]; st < kStep0[k + 1]; ++st) t_step(st);
       }
       // the raw input of chunk ck + 2: loaded here (3 components before its store) rather than at
       // the chunk's start, so its 12 registers are not live beside the transform's row steps
-      if (k == KRRN_W4_RAWK && stage) load_raw(ck + 2, raw);
+      if (k == KRRN_W4_RAWK && stage) {
+        if (KRRN_W4_DMA) dma_raw(ck + 2, p);
+        else load_raw(ck + 2, raw);
+      }
       // issue shape of the slot: the next operands' LDS reads first, then the three MFMAs with the
       // transform VALU in their gaps (one wave's in-order issue would otherwise wait out each
       // dependent MFMA), then the weight reload
@@ -474,10 +504,15 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 #endif
       __builtin_amdgcn_sched_barrier(0);  // keep each component's reload and transform steps in place
     }
-    if (stage) store_raw(p, raw);
+    if (!KRRN_W4_DMA && stage) store_raw(p, raw);
   };
 
   // prologue: raw chunks 0 and 1 to the ring, T(0), weights of chunk 0
+#if KRRN_W4_DMA
+  dma_raw(0, 0);
+  if (nck > 1) dma_raw(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
   {
     f32x4 raw[3];
     load_raw(0, raw);
@@ -487,6 +522,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
       store_raw(1, raw);
     }
   }
+#endif
 #pragma unroll
   for (int k = 0; k < 3; ++k) load_w(0, k);
   __syncthreads();
@@ -499,8 +535,15 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 
   for (int ck = 0; ck < nck; ++ck) {
     do_chunk(ck);
-    // LDS-only hand-offs (ring and V buffers): lgkmcnt, not the in-flight weight loads
+    // hand-offs through LDS: the V buffers (lgkmcnt) and, with LDS-DMA, the raw chunk (this wave's
+    // DMA, issued at the chunk's start: at most the last 3 components' 6 weight loads stay in flight)
+#if KRRN_W4_DMA && KRRN_W4_RAWK >= 6
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * (8 - KRRN_W4_RAWK)) : "memory");
+#elif KRRN_W4_DMA
+    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
   }
 
 #if KRRN_W4_EXP == 5

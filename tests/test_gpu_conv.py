@@ -477,47 +477,6 @@ def test_conv_small(dev, B, cin, cout, H, W, co, nw, ks, k, st):
     assert torch.count_nonzero(out.t[..., np_:]).item() == 0
 
 
-def test_conv_small_group(dev):
-    """krrn_conv_small_group_f32: the four W18 branch shapes (and their (nw, ks) configs) plus a
-    stride-2 and a 1x1 problem in one launch give exactly the single launches' outputs."""
-    from pose_estimation_amd import _lib
-    from pose_estimation_amd.runtime import P, SmallDesc, ptr
-    import ctypes
-    L = _lib.lib()
-    st = P(torch.cuda.current_stream().cuda_stream)
-    B = 6
-    g = torch.Generator().manual_seed(7)
-    for shapes in ([(18, 18, 30, 2, 1, 3, 1), (36, 36, 15, 3, 2, 3, 1), (72, 72, 8, 3, 4, 3, 1),
-                    (144, 144, 4, 3, 4, 3, 1)],
-                   [(20, 36, 30, 3, 2, 3, 2), (72, 20, 8, 2, 4, 1, 1), (36, 72, 15, 3, 4, 3, 2)]):
-        descs, singles = [], []
-        for cin, cout, H, nw, ks, k, s2 in shapes:
-            cp, np_ = ops.pad4(cin), ops.pad4(cout)
-            conv = nn.Conv2d(cin, cout, k, s2, (k - 1) // 2, bias=False)
-            with torch.no_grad():
-                conv.weight.copy_(0.1 * torch.randn(conv.weight.shape, generator=g))
-            spec = ops.make_conv(conv, _bn(cout, g), dev, cin_p=cp)
-            Ho = (H + 2 * ((k - 1) // 2) - k) // s2 + 1
-            xa = _nhwc(torch.randn(B, cin, H, H, generator=g), dev)
-            ra = _nhwc(torch.randn(B, cout, Ho, Ho, generator=g), dev)
-            outs = [torch.full((B, Ho, Ho, np_), float("nan"), device=dev) for _ in range(2)]
-            args = dict(in_=ptr(xa.t), in_cs=xa.cs, in_co=0, B=B, H=H, W=H, cin=cp, wt=ptr(spec.wt[0]), N=np_,
-                        n_store=np_, scale=ptr(spec.scale), bias=ptr(spec.bias), res=ptr(ra.t), res_cs=ra.cs,
-                        res_co=0, out_cs=np_, out_co=0, relu=1, ksize=k, stride=s2, nw=nw, ks=ks)
-            descs.append(SmallDesc(out=ptr(outs[0]), **args))
-            a = dict(args, out=ptr(outs[1]))
-            _lib.check(L.krrn_conv_small_f32(a["in_"], a["in_cs"], 0, B, H, H, cp, a["wt"], np_, np_, a["scale"],
-                                             a["bias"], a["res"], a["res_cs"], 0, a["out"], np_, 0, 1, k, s2, nw, ks,
-                                             st), "small conv")
-            singles.append((outs, spec, xa, ra))
-        arr = (SmallDesc * len(descs))(*descs)
-        _lib.check(L.krrn_conv_small_group_f32(ctypes.cast(arr, P), len(descs), st), "small group")
-        torch.cuda.synchronize()
-        for outs, *_ in singles:
-            assert not torch.isnan(outs[0]).any()
-            assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("B,HW,cin,cout,co,oc,Cx", [(3, 1000, 128, 72, 0, 0, 72), (2, 777, 128, 3, 0, 0, 3),
                                                    (4, 64, 20, 40, 4, 5, 50), (1, 130, 256, 80, 0, 0, 80),
                                                    (2, 1000, 128, 9, 0, 3, 12),

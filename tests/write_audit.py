@@ -139,7 +139,6 @@ def _ptr_value(a, env) -> Optional[int]:
 def op_pointer_sets(op, env, loc: _Locator, host_objs: Dict[int, Any],
                     params: Dict[str, Tuple[List[int], List[int]]]) -> Tuple[set, set]:
     """(region indices the op may write, region indices it only reads)."""
-    from pose_estimation_amd.runtime import ConvDesc, SmallDesc
     w_idx, r_idx = params.get(op.name, ([], []))
     wr, rd = set(), set()
 
@@ -158,7 +157,7 @@ def op_pointer_sets(op, env, loc: _Locator, host_objs: Dict[int, Any],
         if p is None:
             continue
         obj = host_objs.get(p)
-        if obj is not None:  # a krrn_conv_desc / krrn_small_desc array passed by address
+        if obj is not None:  # a krrn_conv_desc array passed by address
             for d in obj:
                 for f in _DESC_OUT:
                     if hasattr(d, f):
@@ -172,7 +171,7 @@ def op_pointer_sets(op, env, loc: _Locator, host_objs: Dict[int, Any],
 
 
 def _host_desc_arrays(plans) -> Dict[int, Any]:
-    from pose_estimation_amd.runtime import ConvDesc, SmallDesc
+    from pose_estimation_amd.runtime import ConvDesc
     out = {}
     for plan in plans:
         stack = list(plan.buffers)
@@ -180,7 +179,7 @@ def _host_desc_arrays(plans) -> Dict[int, Any]:
             x = stack.pop()
             if isinstance(x, (list, tuple)):
                 stack.extend(x)
-            elif isinstance(x, ctypes.Array) and x._type_ in (ConvDesc, SmallDesc):
+            elif isinstance(x, ctypes.Array) and x._type_ is ConvDesc:
                 out[ctypes.addressof(x)] = x
     return out
 
