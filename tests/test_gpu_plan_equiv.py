@@ -1,15 +1,16 @@
 """The forward plan's cross-stream scheduling is bit-neutral.
 
-Five plan-build switches move launches between streams or split them, with the same kernels on the
+Six plan-build switches move launches between streams or split them, with the same kernels on the
 same values, so DESIGN.md section 4 claims bit-identical results for each:
   hrnet.FUSE_EARLY      fuse terms that read one branch start on that branch's stream
   hrnet.MODULE_STREAMS  consecutive HRNet modules keep each branch on its stream (no barrier)
   hrnet.STAGE_STREAMS   HRNet stages chain per branch stream (transitions on their branch's stream)
+  hrnet.FUSE_EDGES      each fuse output waits for its branches through capture edges (no module barrier)
   krrn.FUSION_EARLY     the fusion's cloud-only part runs beside the HRNet phase (stream 7)
   fusion.FUSION_CHUNK   the level-0 GCN GEMM + gather-conv in crop chunks
 A missing dependency in any of them would let a consumer on one stream read a buffer before its
 producer on another stream wrote it: in the tolerance-based parity tests that shows up only as an
-intermittent mismatch. Here one plan is built with all five off (one stream per module, no chunks)
+intermittent mismatch. Here one plan is built with all seven off (one stream per module, no chunks)
 and one with the shipped defaults, and every output of the serial run, the captured graph and a
 replay must be EQUAL (torch.equal), as well as the fusion's level buffers.
 """
@@ -52,7 +53,7 @@ def test_scheduling_switches_are_bit_neutral(dev, monkeypatch):
     assert fusion.FUSION_CHUNK and fusion.FUSION_CHUNK < B
     base_outs, base_bufs = _run(dev, sd, args, perms)
     for name, mod in (("FUSE_EARLY", hrnet), ("MODULE_STREAMS", hrnet), ("STAGE_STREAMS", hrnet),
-                      ("FUSION_EARLY", krrn)):
+                      ("FUSE_EDGES", hrnet), ("FUSION_EARLY", krrn)):
         assert getattr(mod, name), name  # the shipped default is on
         monkeypatch.setattr(mod, name, False)
     monkeypatch.setattr(fusion, "FUSION_CHUNK", 0)
