@@ -21,24 +21,28 @@
 // for all 64 output channels of the block, by the block cooperatively, into LDS:
 //
 //   block = 16 x 2 tiles (64 x 8 output pixels of one image) x 64 output channels, 512 threads.
-//   Per 8-channel chunk ck:
-//     raw  : the 10 x 66 x 8 input region is loaded to registers (3 b128 per thread) and stored to
-//            a 2-slot LDS ring, one chunk ahead (padded slots: conflict-free patch reads);
-//     T    : waves 0..5 each own one column v of the 6x6 transform: lane (tile, channel half h)
-//            forms e[r] = B_v(d[r][.]) for the 6 patch rows, then V[u][v] = B_u(e[.]) for the 6 u,
-//            splits each into the three bf16 terms and writes the MFMA operand chain
-//            [V_m V_h | V_l] (b128 + b64) to a 2-slot V buffer; V[comp][h][tile] = lane order, so
-//            the consumer's read is the producer's write address;
+//   Per 8-channel chunk ck (one barrier per chunk):
+//     raw  : the 10 x 66 x 8 input region of chunk ck + 2 goes by LDS-DMA (3 buffer_load ... lds
+//            per wave, no staging registers) into a 2-slot ring (padded slots: conflict-free patch
+//            reads), requested after component 6 of chunk ck;
+//     T    : the transform of chunk ck + 1, interleaved with M(ck) (its steps sit in the MFMA gaps of
+//            each component): waves 0..3 own columns v = 0..3 of the 6x6 transform, waves 4 / 6 and
+//            5 / 7 columns 4 and 5 (each pair splitting the column's 6 outputs); lane (tile, channel
+//            half h) forms e[r] = B_v(d[r][.]) for the 6 patch rows, then V[u][v] = B_u(e[.]), splits
+//            each into the three bf16 terms and writes the MFMA operand chain [V_m V_h | V_l]
+//            (b128 + b64) to a 2-slot V buffer; V[comp][h][tile] = lane order, so the consumer's read
+//            is the producer's write address;
 //     M    : wave (g = wave & 3, nh = wave >> 2) owns the 3x3 component sub-grid g
 //            (u in 3(g>>1)+0..2, v in 3(g&1)+0..2) for output channels 32 nh .. +31: per component
-//            one b128 + one b64 V read, three v_mfma_f32_32x32x16_bf16 (mm+hh, mh+hl, hm+lh as in
-//            winograd.hip), then that component's weights for chunk ck+1 are loaded into the same
-//            registers.
-//     Waves 0..3 run M(ck) then T(ck+1), waves 4..7 T(ck+1) then M(ck): the two waves of a SIMD
-//     (w, w+4) put their VALU transform beside the other's MFMAs. One barrier per chunk.
-//   Epilogue: 4 rounds of 8 tiles: each wave writes its accumulators to LDS as [comp][n][tile], then
-//   thread (n, tile quad, output row i) forms t[v] = A_i(M[.][v]) and Y[i][j] = A_j(t), applies
-//   BN / bias / residual / ReLU and stores: lanes run over channels (256-B store runs).
+//            one b128 + one b64 V read (one component ahead), three v_mfma_f32_32x32x16_bf16
+//            (mm+hh, mh+hl, hm+lh as in winograd.hip), then the weights of the component 3 ahead
+//            are loaded into a rolling 3-component register buffer.
+//   Epilogue: 2 passes of 16 tiles through LDS ([comp][tile][n]); thread (channel quad, tile, output
+//   row i) forms t[v] = A_i(M[.][v]) and Y[i][j] = A_j(t), applies BN / bias / residual / ReLU and
+//   stores float4 channel runs.
+// Where the time goes (profiles/w4_trace.py, per-wave cycle stamps): the chunk
+// loop 75 %, the epilogue 14 % (VALU-bound A^T transform), the prologue 8 %; the chip runs at
+// ~1.5 GHz under this kernel against ~2.1 GHz with either the MFMAs or the transform removed.
 #include <type_traits>
 
 #include "krrn_common.h"
@@ -63,23 +67,16 @@ constexpr int kVMH = 36 * 64 * 4;                 // u32 per V buffer, plane [V_
 constexpr int kVL = 36 * 64 * 2;                  // u32 per V buffer, plane [V_l]
 constexpr int kET = kN * 4;                       // epilogue bytes per (component, tile): [64 n] f32
 constexpr unsigned kOOB = 0xFFFF0000u;
-// timing experiments only (results wrong; profiles/build_variant.sh): 1 no MFMAs, 2 no weight reloads,
-// 3 no transform, 4 no raw staging after the prologue, 5 no epilogue
+// timing experiments only (results wrong; profiles/build_variant.sh), a bit mask: 1 no MFMAs, 2 no weight reloads,
+// 4 no transform, 8 no raw staging after the prologue, 16 no epilogue, 32 no output stores
 #ifndef KRRN_W4_EXP
 #define KRRN_W4_EXP 0
 #endif
-#ifndef KRRN_W4_DMA
-#define KRRN_W4_DMA 1  // raw staging by LDS-DMA (0: through registers)
+#ifndef KRRN_W4_TRACE
+#define KRRN_W4_TRACE 0  // 1: per-wave cycle stamps of the first 256 blocks (profiles/w4_trace.py; timing study only)
 #endif
-#ifndef KRRN_W4_TDUP
-#define KRRN_W4_TDUP 0  // 1: waves 6, 7 repeat columns 4, 5 (one code path, 5 % slower); 0: they and the last chunk skip it
-#endif
-#ifndef KRRN_W4_RAWK
-#define KRRN_W4_RAWK 6  // component slot after which the next raw chunk is loaded (-1: chunk start)
-#endif
-#ifndef KRRN_W4_GAP
-#define KRRN_W4_GAP 6  // transform VALU instructions placed in each MFMA gap
-#endif
+constexpr int kRawK = 6;  // component slot after which the raw chunk two ahead is requested
+constexpr int kGap = 6;   // transform VALU instructions placed in each MFMA gap
 static_assert(kRR * kRS <= kRing && kRing == 3 * 512, "raw ring");
 static_assert(2 * (kRC - 1) + 1 + (kRC - 1) / 4 < kRS && (kRS * 4) % 16 == 0, "padded raw row");
 // LDS bytes: V plane MH x 2 | V plane L x 2 | raw ring x 2 (the epilogue's [36][64][12] f32 reuses
@@ -259,7 +256,7 @@ __device__ __forceinline__ void epi_row(const Wino4Args& a, const char* E, int n
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
       }
-      *reinterpret_cast<f32x4*>(o + j * a.out_cs) = v;
+      if (!(KRRN_W4_EXP & 32) || v[0] == 1234.5f) *reinterpret_cast<f32x4*>(o + j * a.out_cs) = v;
     }
     return;
   }
@@ -292,11 +289,29 @@ __global__ __launch_bounds__(256) void wino4_head_finish_kernel(const float* __r
     if (o < p1) out[(b * out_c + o) * HW + p] = v[o] + (b1 ? b1[o] : 0.f);
 }
 
+#if KRRN_W4_TRACE
+constexpr int kTrN = 52;  // per wave: [16 chunks][start, after component 4, before the barrier], 4 more
+__device__ unsigned g_w4_trace[256 * 8 * kTrN];
+#define W4_MARK(i)                                                  \
+  do {                                                              \
+    const unsigned t_ = (unsigned)__builtin_readcyclecounter();     \
+    if (lane == 0 && (i) < kTrN) trace_lds[wave * kTrN + (i)] = t_; \
+  } while (0)
+#else
+#define W4_MARK(i) \
+  do {             \
+  } while (0)
+#endif
+
 template <bool HEAD>
 __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#if KRRN_W4_TRACE
+  __shared__ unsigned trace_lds[8 * kTrN];
+#endif
+  W4_MARK(48);
   const int gxn = krrn_cdiv(a.Wt, kGX), gyn = krrn_cdiv(a.Ht, kGY), nbn = krrn_cdiv(a.N, kN);
   const int per_img = gxn * gyn;
   const int bid = krrn_xcd_remap(blockIdx.x, a.B * per_img * nbn);
@@ -314,11 +329,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   unsigned roff[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-#if KRRN_W4_DMA
     const int s = 192 * wave + 64 * i + lane;  // LDS-DMA: wave instruction i fills slots 64 (3 wave + i) ..
-#else
-    const int s = tid + 512 * i;
-#endif
     const int r = s / kRS, q = s - (s / kRS) * kRS;
     const int g4 = q / 9, w9 = q - (q / 9) * 9;
     const int col = 4 * g4 + (w9 >> 1), hh = w9 & 1;
@@ -326,11 +337,6 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     const bool ok = r < kRR && w9 < 8 && col < kRC && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
     roff[i] = ok ? (unsigned)((((long long)iy * a.W + ix) * a.in_cs + 4 * hh) * 4) : kOOB;
   }
-  auto load_raw = [&](int ck, f32x4 (&raw)[3]) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-      raw[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, roff[i], ck * kC * 4, 0));
-  };
   // raw chunk ck straight into ring slot `slot` by LDS-DMA (buffer_load_dwordx4 ... lds: 1 KB per
   // wave instruction, no staging registers); padding slots receive zeros
   auto dma_raw = [&](int ck, int slot) {
@@ -339,11 +345,6 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     for (int i = 0; i < 3; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(dst + 1024 * i), 16,
                                                roff[i], ck * kC * 4, 0, 0);
-  };
-  auto store_raw = [&](int slot, const f32x4 (&raw)[3]) {
-    char* dst = smem + kOffR + slot * (kRingF * 4) + 16 * tid;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) *reinterpret_cast<f32x4*>(dst + 8192 * i) = raw[i];
   };
 
   // M: wave (g, nh), components (u, v) = (3 (g >> 1) + k / 3, 3 (g & 1) + k % 3), k = 0..8
@@ -379,9 +380,11 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   // forms e[r] = B_tv(d[r][.]) over the 6 patch rows (the row's taps: up to 4 columns with
   // wave-uniform coefficients), then V[u][tv] = B_u(e) for u = 0..5, split into the operand chain
   // and written to the V buffer at (6u + tv, h, tile) = the M phase's read address.
-  // waves 6 and 7 repeat columns 4 and 5 (the same values to the same addresses): every wave runs
-  // one code path, so the transform VALU can sit in the MFMA gaps of the same basic block
-  const int tv = wave < 6 ? wave : wave - 2;
+  // balanced over the SIMDs (waves w and w + 4 share one): waves 0..3 transform columns 0..3 whole,
+  // waves 4 / 6 column 4 and waves 5 / 7 column 5, each pair splitting its 6 outputs (u < 3 / u >= 3)
+  // and both doing the column's 6 row steps: 326 + 211 VALU per SIMD instead of 326 + 326 / 326
+  const int tv = wave < 4 ? wave : 4 + (wave & 1);
+  const int tulo = wave < 6 ? 0 : 3, tuhi = wave < 4 ? 6 : (wave < 6 ? 3 : 6);
   int tcol[4];
   float tk[4];
   switch (tv) {
@@ -422,6 +425,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
       return;
     }
     const int u = s - 6;
+    if (u < tulo || u >= tuhi) return;
     f32x4 x;
     switch (u) {
       case 0: x = bt_row<0>(te); break;
@@ -442,11 +446,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   // one chunk: M(ck) on V[ck & 1], interleaved with T(ck + 1) into V[(ck + 1) & 1]; the raw input
   // of chunk ck + 2 goes into the ring slot T(ck) has read
   auto do_chunk = [&](int ck) {
-#if KRRN_W4_TDUP
-    constexpr bool tr = KRRN_W4_EXP != 3;
-#else
-    const bool tr = KRRN_W4_EXP != 3 && wave < 6 && ck + 1 < nck;  // waves 6, 7 and the last chunk: no T
-#endif
+    const bool tr = !(KRRN_W4_EXP & 4) && ck + 1 < nck;  // the last chunk: no T
     const int p = ck & 1;
     const char* vm = smem + p * (kVMH * 4) + 16 * lane;
     const char* vlo = smem + kOffL + p * (kVL * 4) + 8 * lane;
@@ -455,12 +455,8 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
       const u32x2 l = *reinterpret_cast<const u32x2*>(vlo + comp_of(k) * 512);
       return u32x6{mh[0], mh[1], mh[2], mh[3], l[0], l[1]};
     };
-    f32x4 raw[3];
-    const bool stage = ck + 2 < nck && KRRN_W4_EXP != 4;
-#if KRRN_W4_DMA
-    if (KRRN_W4_RAWK < 0 && stage) dma_raw(ck + 2, p);  // into the slot T(ck) read during chunk ck - 1
+    const bool stage = ck + 2 < nck && !(KRRN_W4_EXP & 8);
     __builtin_amdgcn_sched_barrier(0);
-#endif
     if (tr) t_begin(ck + 1 < nck ? ck + 1 : ck + 1 - 2);  // past the last chunk: a harmless repeat
     u32x6 acn = chain(0);
 #pragma unroll
@@ -470,83 +466,64 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
       asm volatile("" : "+v"(ac));  // one register tuple: the MFMA operands are its sub-registers
       u32x6 bc = {wmh[k % 3][0], wmh[k % 3][1], wmh[k % 3][2], wmh[k % 3][3], wl[k % 3][0], wl[k % 3][1]};
       asm volatile("" : "+v"(bc));
-#if KRRN_W4_EXP == 1
+#if KRRN_W4_EXP & 1
       acc[k][0] += __uint_as_float(ac[0] ^ ac[4] ^ bc[0] ^ bc[4]);
 #else
       acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 0), acc[k], 0, 0, 0);  // mm + hh
       acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 0), sub4(bc, 2), acc[k], 0, 0, 0);  // mh + hl
       acc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sub4(ac, 2), sub4(bc, 0), acc[k], 0, 0, 0);  // hm + lh
 #endif
-#if KRRN_W4_EXP != 2
+#if !(KRRN_W4_EXP & 2)
       if (k < 6) load_w(ck, k + 3); else load_w(ck + 1, k - 6);
 #endif
       if (tr) {
 #pragma unroll
         for (int st = kStep0[k]; st < kStep0[k + 1]; ++st) t_step(st);
       }
-      // the raw input of chunk ck + 2: loaded here (3 components before its store) rather than at
-      // the chunk's start, so its 12 registers are not live beside the transform's row steps
-      if (k == KRRN_W4_RAWK && stage) {
-        if (KRRN_W4_DMA) dma_raw(ck + 2, p);
-        else load_raw(ck + 2, raw);
-      }
+      // the raw input of chunk ck + 2, into the ring slot T(ck) read during chunk ck - 1 (requested at
+      // the chunk's start instead, it only moves the wait: profiles/w4_trace.py)
+      if (k == 4 && ck < 16) W4_MARK(3 * ck + 1);
+      if (k == kRawK && stage) dma_raw(ck + 2, p);
       // issue shape of the slot: the next operands' LDS reads first, then the three MFMAs with the
       // transform VALU in their gaps (one wave's in-order issue would otherwise wait out each
       // dependent MFMA), then the weight reload
-#if KRRN_W4_GAP > 0
       __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // DS reads
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, KRRN_W4_GAP, 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x002, kGap, 0);  // VALU
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, KRRN_W4_GAP, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, kGap, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, KRRN_W4_GAP, 0);
-#endif
+      __builtin_amdgcn_sched_group_barrier(0x002, kGap, 0);
       __builtin_amdgcn_sched_barrier(0);  // keep each component's reload and transform steps in place
     }
-    if (!KRRN_W4_DMA && stage) store_raw(p, raw);
   };
 
   // prologue: raw chunks 0 and 1 to the ring, T(0), weights of chunk 0
-#if KRRN_W4_DMA
   dma_raw(0, 0);
   if (nck > 1) dma_raw(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-  {
-    f32x4 raw[3];
-    load_raw(0, raw);
-    store_raw(0, raw);
-    if (nck > 1) {
-      load_raw(1, raw);
-      store_raw(1, raw);
-    }
-  }
-#endif
 #pragma unroll
   for (int k = 0; k < 3; ++k) load_w(0, k);
   __syncthreads();
-  if (KRRN_W4_EXP != 3) {
+  if (!(KRRN_W4_EXP & 4)) {
     t_begin(0);
 #pragma unroll
     for (int st = 0; st < 12; ++st) t_step(st);
   }
   __syncthreads();
 
+  W4_MARK(49);
   for (int ck = 0; ck < nck; ++ck) {
+    if (ck < 16) W4_MARK(3 * ck);
     do_chunk(ck);
-    // hand-offs through LDS: the V buffers (lgkmcnt) and, with LDS-DMA, the raw chunk (this wave's
-    // DMA, issued at the chunk's start: at most the last 3 components' 6 weight loads stay in flight)
-#if KRRN_W4_DMA && KRRN_W4_RAWK >= 6
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * (8 - KRRN_W4_RAWK)) : "memory");
-#elif KRRN_W4_DMA
-    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
+    if (ck < 16) W4_MARK(3 * ck + 2);
+    // hand-offs through LDS: the V buffers (lgkmcnt) and the raw chunk this wave's DMA wrote (issued
+    // after component kRawK: the 2 (b128 + b64) weight loads of each later component may stay in flight)
+    static_assert(kRawK >= 6 && kRawK <= 8, "vmcnt count below");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * (8 - kRawK)) : "memory");
   }
 
-#if KRRN_W4_EXP == 5
+#if KRRN_W4_EXP & 16
   {
     float sum = 0.f;
 #pragma unroll
@@ -559,6 +536,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   // (r & 3) + 8 ((r >> 2) & 1) + 4 h of the pass); a pass's stores free its 72 accumulator registers.
   // Then wave w forms output row i = w & 3 of tile groups (w >> 2) and (w >> 2) + 2: lane (tile of
   // the group, channel quad) -> float4 channel-run stores.
+  W4_MARK(50);
   const int enq = lane & 15, etl = lane >> 4, ei = wave & 3;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
@@ -587,9 +565,21 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     }
     __syncthreads();
   }
+#if KRRN_W4_TRACE
+  W4_MARK(51);
+  __syncthreads();
+  if (blockIdx.x < 256)
+    for (int i = tid; i < 8 * kTrN; i += 512) g_w4_trace[blockIdx.x * 8 * kTrN + i] = trace_lds[i];
+#endif
 }
 
 }  // namespace
+
+#if KRRN_W4_TRACE
+KRRN_API int krrn_w4_trace_copy(void* dst) {  // 256 blocks x 8 waves x kTrN u32 cycle stamps
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_w4_trace), sizeof(g_w4_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 KRRN_API int krrn_conv3x3_wino4_x3_f32(const float* in, int in_cs, int in_co, int B, int H, int W, int cin,
                                        const void* U3, int N, int n_store, const float* scale, const float* bias,
