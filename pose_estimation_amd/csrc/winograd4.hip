@@ -498,19 +498,23 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     }
   };
 
-  // prologue: raw chunks 0 and 1 to the ring, T(0), weights of chunk 0
+  // prologue: raw chunks 0 and 1 to the ring and chunk 0's first weights requested together; T(0)
+  // waits only for raw chunk 0 (in-order vmcnt: chunk 1's 3 DMAs and the 6 weight loads may still
+  // be in flight), chunk 1 lands under it
   dma_raw(0, 0);
   if (nck > 1) dma_raw(1, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int k = 0; k < 3; ++k) load_w(0, k);
-  __syncthreads();
+  if (nck > 1)
+    asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
   if (!(KRRN_W4_EXP & 4)) {
     t_begin(0);
 #pragma unroll
     for (int st = 0; st < 12; ++st) t_step(st);
   }
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   W4_MARK(49);
   for (int ck = 0; ck < nck; ++ck) {
