@@ -104,6 +104,20 @@ int krrn_conv2d_x3_f32(const float* in, int in_cs, int in_co, int B, int Hi, int
                        int res_cs, int res_co, float* out, int out_cs, int out_co, int Ho, int Wo, int osy, int osx,
                        int ooy, int oox, int relu, int tile, int splits, float* workspace, void* stream);
 int krrn_conv2d_group_x3_f32(const krrn_conv_desc* descs, int n, int tile, void* stream);
+/* Stride-2 ConvTranspose2d (kernel <= 4, padding 1; myhrnet.py:314-326's deconv, krrn.py:47-49's
+ * XYZNet layer) as its four output parity classes in ONE block per 4 x 32 region of the input grid, on
+ * split-bf16 operands at f32 accuracy (convt.hip): out[2a + py][2b + px][n] (NHWC, channels out_co ..
+ * out_co + N - 1 of pixel rows of out_cs floats, Ho x Wo <= 2 Hi x 2 Wi) = act(scale[n] *
+ * sum over the class's taps t and channels k of in[a + dy_t][b + dx_t][k] W[k][n] + bias[n]).
+ * cls_taps (host memory, read at the call): for class c = 2 py + px, cls_taps[5c] = its tap count
+ * (1..4) and cls_taps[5c + 1 + t] = (dy_t + 1) * 3 + (dx_t + 1). U3 = ops.convT_weights_x3: plane
+ * U_mh [cin/8][16][N][2][8] bf16 (element class * 4 + tap; m0..m3 h0..h3 of channels 4 half ..
+ * 4 half + 3) then plane U_l [cin/8][16][N][2][4]; 16-byte aligned. N = 128; cin a multiple of 8;
+ * in 16-byte aligned with in_cs, in_co multiples of 4. relu != 0 applies ReLU. Replaces the grouped
+ * krrn_conv2d_group_x3_f32 launch of the four classes (lib/network/krrn.py:47-49). */
+int krrn_convT_s2_x3_f32(const float* in, int in_cs, int in_co, int B, int Hi, int Wi, int cin, const int* cls_taps,
+                         const void* U3, int N, const float* scale, const float* bias, int relu, float* out,
+                         int out_cs, int out_co, int Ho, int Wo, void* stream);
 
 /* Plain f32 GEMM on hipBLASLt (library-shaped GEMMs of the fusion / TBase, see blas.hip):
  *   out[m*ldo + n] = act(sum_k A[m*lda + k] W[n*K + k] + bias[n] + res[m*ldr + n]),  0 <= n < N

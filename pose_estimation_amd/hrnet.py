@@ -33,6 +33,7 @@ from .runtime import add_conv_group, add_gemm, Plan, add_conv, ptr
 # switches (pose_estimation_amd/knobs.py has each one's meaning)
 DECONV_FOLD = knobs.flag("KRRN_DECONV_FOLD")
 CONVT_GROUP = knobs.flag("KRRN_CONVT_GROUP")
+CONVT_S2 = knobs.flag("KRRN_CONVT_S2")
 SMALL_CONV = knobs.flag("KRRN_SMALL_CONV")
 GEMM_1X1 = knobs.flag("KRRN_GEMM_1X1")
 FUSE_ID_FIRST = knobs.flag("KRRN_FUSE_ID_FIRST")
@@ -375,8 +376,26 @@ class _Builder:
                       res.cs if res is not None else 0, res.co if res is not None else 0, ptr(out.t), out.cs,
                       out.co, int(relu), meta=meta)
 
+    def emit_convT_s2(self, x: Act, spec, out: Act, relu: bool, tag: str = "conv"):
+        """A stride-2 transposed conv with 128 outputs (the deconv, myhrnet.py:314-326; XYZNet's first
+        layer, krrn.py:47-49) as ONE krrn_convT_s2_x3_f32 launch: all four parity classes of a 4 x 32
+        input-grid region per block, the input staged and split once per 8-channel chunk."""
+        U3, table = ops.convT_weights_x3(spec)
+        self.specs.append(U3)
+        taps = sum(len(t) for t in spec.taps)
+        grid = x.B * (-(-x.H // 4) * 4) * (-(-x.W // 32) * 32)  # the blocks' padded input grid
+        issued = 2.0 * grid * 128 * spec.cin_p * max(len(t) for t in spec.taps) * 4  # the busiest class sets the pace
+        meta = dict(kernel="convt_s2_x3", flops=2.0 * spec.cin * spec.cout * taps * x.B * x.H * x.W,
+                    tag=tag + "_convT", M=x.B * x.H * x.W * 4, N=128, K=spec.cin_p * taps,
+                    mfma_flops=issued * 6 / 16, mfma_bf16_flops=issued * 6)
+        self.plan.add("krrn_convT_s2_x3_f32", ptr(x.t), x.cs, x.co, x.B, x.H, x.W, spec.cin_p, table, ptr(U3), 128,
+                      ptr(spec.scale), ptr(spec.bias), int(relu), ptr(out.t), out.cs, out.co, out.H, out.W, meta=meta)
+
     def emit_conv(self, x: Act, spec, out: Act, res: Optional[Act], relu: bool, tag: str = "conv"):
         np_ = pad4(spec.cout)
+        if CONVT_S2 and ops.convT_s2_eligible(spec, x, out, res):
+            self.emit_convT_s2(x, spec, out, relu, tag)
+            return
         if spec.kind == "convT" and CONVT_GROUP and 1 < len(spec.taps) <= 4:
             # the parity classes write disjoint output pixels: one grouped launch (no tail per class)
             probs = [dict(x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=x.H, Wg=x.W,

@@ -293,6 +293,34 @@ def wino_weights_x3(U: torch.Tensor) -> torch.Tensor:
     return torch.cat([mh, l.reshape(-1)]).contiguous()
 
 
+def convT_s2_eligible(spec: "ConvSpec", x, out, res) -> bool:
+    """krrn_convT_s2_x3_f32 runs a stride-2 transposed conv with 128 outputs, taps within one input
+    pixel of the grid point (padding 1, kernel <= 4), >= 8 input channels in whole chunks of 8, a
+    16-byte aligned NHWC input and no residual: the backbone's deconv and XYZNet's first layer."""
+    return (spec.kind == "convT" and len(spec.taps) == 4 and pad4(spec.cout) == 128 and res is None
+            and all(1 <= len(t) <= 4 and all(-1 <= dy <= 1 and -1 <= dx <= 1 for dy, dx in t) for t in spec.taps)
+            and spec.cin_p % 8 == 0 and x.cs % 4 == 0 and x.co % 4 == 0 and x.co + spec.cin_p <= x.cs
+            and out.co + 128 <= out.cs and out.H <= 2 * x.H and out.W <= 2 * x.W
+            and [tuple(o) for o in spec.cls_off] == [(0, 0), (0, 1), (1, 0), (1, 1)])
+
+
+def convT_weights_x3(spec: "ConvSpec") -> Tuple[torch.Tensor, "ctypes.Array"]:
+    """make_convT's per-class weights [N][taps * cin_p] -> (U3, cls_taps) for krrn_convT_s2_x3_f32:
+    U [cin_p / 8][class * 4 + tap][N][8] f32 (zero for a class's missing taps) split into the
+    wino_weights_x3 planes, and the 4 x 5 int table [tap count, (dy + 1) * 3 + (dx + 1) ...]."""
+    N, cin_p = spec.wt[0].shape[0], spec.cin_p
+    nck = cin_p // 8
+    U = torch.zeros(nck, 16, N, 8, device=spec.wt[0].device)
+    table = (ctypes.c_int * 20)()
+    for c, taps in enumerate(spec.taps):
+        w = spec.wt[c].float().reshape(N, len(taps), nck, 8)
+        table[5 * c] = len(taps)
+        for t, (dy, dx) in enumerate(taps):
+            U[:, 4 * c + t] = w[:, t].permute(1, 0, 2)
+            table[5 * c + 1 + t] = (dy + 1) * 3 + (dx + 1)
+    return wino_weights_x3(U), table
+
+
 def conv_weights_x3(wt: torch.Tensor) -> torch.Tensor:
     """krrn_conv2d_f32 weights [N][K] f32 -> the split chains krrn_conv2d_x3_f32 reads: bf16
     [N][K / 4][16], per 4 k the terms m0..m3 h0..h3 l0..l3 then 4 zeros (K a multiple of 4)."""

@@ -49,6 +49,7 @@ _lib.register("krrn_conv2d_x3_f32", [P, I, I, I, I, I, I, I, I, I, I, P, P, P, I
 _lib.register("krrn_conv3x3_wino_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv3x3_wino_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
 _lib.register("krrn_conv3x3_wino4_x3_f32", [P, I, I, I, I, I, I, P, I, I, P, P, P, I, I, P, I, I, I, P])
+_lib.register("krrn_convT_s2_x3_f32", [P, I, I, I, I, I, I, P, P, I, P, P, I, P, I, I, I, I, P])
 _lib.register("krrn_conv3x3_wino_x3_head_f32", [P, I, I, I, I, I, I, P, I, P, P, P, I, I, I, P, P, I, P, P, I, P])
 _lib.register("krrn_conv3x3_wino4_x3_head_f32", [P, I, I, I, I, I, I, P, I, P, P, P, I, I, I, P, P, I, P, P, I, P])
 _lib.register("krrn_conv1x1_nchw_f32", [P, I, I, I, I, I, P, I, I, P, P, P, I, I, P])

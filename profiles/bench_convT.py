@@ -2,7 +2,8 @@
 128 -> 128, both 30 -> 60 px, B = 64) as one grouped split-bf16 launch per tile shape, built the
 way hrnet.emit_conv builds them (parity classes, channel-chunk k order).
 
-usage (GPU box): python3 profiles/bench_convT.py
+usage (GPU box): python3 profiles/bench_convT.py   (TILES=1,6,8 the grouped tiles; "s2" = the
+all-classes-per-block kernel, krrn_convT_s2_x3_f32)
 """
 import os
 import sys
@@ -58,12 +59,28 @@ for name, conv in cases:
     xa.t.copy_(torch.randn(xa.t.shape, generator=g).to(dev))
     out = ops.new_act(B, 60, 60, spec.cout, dev)
     line, ref = name + ":", None
-    for tile in (1, 6, 8):
+    for tile in [int(t) for t in os.environ.get("TILES", "1,6,8").split(",")]:
         for q in (0, 16):
-            plan = build(spec, xa, out, tile, q)
-            ms = ev_time(lambda: plan.run({}))
+            try:
+                plan = build(spec, xa, out, tile, q)
+                ms = ev_time(lambda: plan.run({}))
+            except RuntimeError as e:
+                line += f" | t{tile} q{q} n/a ({str(e).split(': ')[-1][:24]})"
+                continue
             got = out.t.clone()
             ref = got if ref is None else ref
             err = float((got - ref).abs().max() / ref.abs().max())
             line += f" | t{tile} q{q} {ms * 1e3:6.1f} us ({err:.1e})"
+    U3, table = ops.convT_weights_x3(spec)
+    from pose_estimation_amd import _lib  # noqa: E402
+    from pose_estimation_amd.runtime import P  # noqa: E402
+
+    def s2():
+        _lib.check(_lib.lib().krrn_convT_s2_x3_f32(ptr(xa.t), xa.cs, xa.co, B, 30, 30, spec.cin_p, table, ptr(U3), 128,
+                                                   ptr(spec.scale), ptr(spec.bias), 1, ptr(out.t), out.cs, out.co,
+                                                   60, 60, P(torch.cuda.current_stream().cuda_stream)), "convT_s2")
+    ms = ev_time(s2)
+    got = out.t.clone()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    line += f" | s2 {ms * 1e3:6.1f} us ({err:.1e})"
     print(line, flush=True)

@@ -342,6 +342,73 @@ def test_conv3x3_winograd(dev, cin, cout, H, W, co):
     torch.testing.assert_close(got3, got, rtol=1e-5, atol=2e-6 * scale)
 
 
+@pytest.mark.parametrize("cin,k,op,H,W,ci,co,relu,bias", [
+    (272, 4, 0, 30, 30, 0, 0, 1, False),  # the folded deconv (myhrnet.py:314-326)
+    (128, 3, 1, 30, 30, 0, 0, 1, False),  # XYZNet's first layer (krrn.py:47-49)
+    (64, 4, 0, 13, 37, 4, 8, 0, True),    # ragged: rows not a multiple of 4, two 32-column blocks
+    (8, 3, 1, 5, 3, 0, 4, 1, True),       # one chunk, a tiny grid (halo everywhere)
+    (24, 2, 0, 9, 33, 0, 0, 1, False)])   # kernel 2: one tap per class, 2H - 2 output rows
+def test_convT_s2(dev, cin, k, op, H, W, ci, co, relu, bias):
+    """Stride-2 transposed conv, all four parity classes per block (krrn_convT_s2_x3_f32, convt.hip),
+    channel-offset input / output, BN (+ conv bias), ReLU: vs torch fp32 (TOL), vs an f64 transposed
+    conv (max |err| <= 2e-6 max |ref|: the split-bf16 products at f32 accuracy), and vs the grouped
+    implicit GEMM it replaces (krrn_conv2d_group_x3_f32: same products, another summation order).
+    NaN-filled output: every pixel and channel it owns is written, the channels past it untouched."""
+    from pose_estimation_amd import _lib
+    from pose_estimation_amd.runtime import P, add_conv_group, Plan, ptr
+    g = torch.Generator().manual_seed(cin + k + H + W)
+    B, cout = 3, 128
+    convT = nn.ConvTranspose2d(cin, cout, k, 2, 1, output_padding=op, bias=bias)
+    with torch.no_grad():
+        convT.weight.copy_(torch.randn(convT.weight.shape, generator=g) / (2.0 * cin ** 0.5))
+        if bias:
+            convT.bias.copy_(0.1 * torch.randn(cout, generator=g))
+    bn = _bn(cout, g)
+    x = torch.randn(B, cin, H, W, generator=g)
+    act = torch.relu if relu else (lambda t: t)
+    ref = act(bn(convT(x))).detach()
+    with torch.no_grad():
+        s64 = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+        y64 = F.conv_transpose2d(x.double(), convT.weight.double(), convT.bias.double() if bias else None,
+                                 stride=2, padding=1, output_padding=op)
+        ref64 = act((y64 - bn.running_mean.double()[:, None, None]) * s64[:, None, None]
+                    + bn.bias.double()[:, None, None])
+    Ho, Wo = ref.shape[2:]
+    xa = _nhwc(x, dev, cs=cin + ci + 4, co=ci)
+    spec = ops.make_convT(convT, bn, dev)
+    U3, table = ops.convT_weights_x3(spec)
+    out = ops.new_act(B, Ho, Wo, cout, dev, cs=cout + co + 4)
+    out.t.fill_(float("nan"))
+    _lib.check(_lib.lib().krrn_convT_s2_x3_f32(ptr(xa.t), xa.cs, xa.co, B, H, W, spec.cin_p, table, ptr(U3), cout,
+                                               ptr(spec.scale), ptr(spec.bias), relu, ptr(out.t), out.cs, co, Ho,
+                                               Wo, P(torch.cuda.current_stream().cuda_stream)), "convT_s2")
+    torch.cuda.synchronize()
+    t = out.t.cpu()
+    assert torch.isnan(t[..., :co]).all() and torch.isnan(t[..., co + cout:]).all()
+    got = t[..., co:co + cout].permute(0, 3, 1, 2)
+    assert not torch.isnan(got).any()
+    torch.testing.assert_close(got, ref, **TOL)
+    err = float((got.double() - ref64).abs().max() / ref64.abs().max())
+    assert err <= 2e-6, err
+    if (Ho, Wo) != (2 * H, 2 * W):
+        return  # the grouped launch below covers the whole 2H x 2W class grid (the model's convTs)
+    # the grouped implicit GEMM on the same input
+    grp = ops.new_act(B, Ho, Wo, cout, dev)
+    plan, keep = Plan(dev), []
+    probs = []
+    for w, taps, (ooy, oox) in zip(spec.wt, spec.taps, spec.cls_off):
+        keep.append(ops.conv_weights_x3(w))
+        probs.append(dict(x=ptr(xa.t), x_cs=xa.cs, x_co=xa.co, B=B, Hi=H, Wi=W, cin_p=spec.cin_p, Hg=H, Wg=W, in_s=1,
+                          taps=taps, wt=ptr(keep[-1]), N=cout, n_store=cout, scale=ptr(spec.scale),
+                          bias=ptr(spec.bias), out=ptr(grp.t), out_cs=grp.cs, out_co=0, Ho=Ho, Wo=Wo, osy=2, osx=2,
+                          ooy=ooy, oox=oox, relu=bool(relu), cin=cin, cout=cout))
+    add_conv_group(plan, probs, tile=1, x3=True)
+    plan.run({})
+    torch.cuda.synchronize()
+    torch.testing.assert_close(got, grp.t[..., :cout].permute(0, 3, 1, 2).cpu(), rtol=1e-5,
+                               atol=2e-6 * float(ref.abs().max()))
+
+
 @pytest.mark.parametrize("cin,cout,H,W,co,relu", [(128, 128, 32, 40, 0, 1), (64, 72, 33, 37, 4, 1),
                                                   (96, 128, 35, 64, 8, 0), (128, 64, 60, 60, 0, 1),
                                                   (128, 128, 120, 120, 0, 1)])
