@@ -83,7 +83,7 @@ def roofline_from_profile(prof, B: int):
     achieved = (g["flops"] / g["n"]) / (avg_ms * 1e-3) / 1e12 if g["flops"] > 0 else None
     conv_ms = sum(v["ms"] for k, v in groups.items() if k.startswith("conv_gemm"))
     conv_fl = sum(v["flops"] for k, v in groups.items() if k.startswith("conv_gemm"))
-    allc = [v for k, v in groups.items() if k.startswith(("conv_gemm", "conv_group", "wino", "hipblaslt"))]
+    allc = [v for k, v in groups.items() if k.startswith(("conv_gemm", "conv_group", "convt", "wino", "hipblaslt"))]
     allc_ms, allc_fl, allc_mf = (sum(v[f] for v in allc) for f in ("ms", "flops", "mfma"))
     breakdown = {k: {"ms": round(v["ms"], 4), "launches": v["n"],
                      **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {})}
