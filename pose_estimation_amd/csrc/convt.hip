@@ -166,7 +166,6 @@ __global__ __launch_bounds__(512, 1) void convt_s2_x3_kernel(const ConvTArgs a) 
   f32x4 raw = load_raw(1);  // chunk 1 (past the last chunk: a harmless repeat of it)
   __syncthreads();
 
-  const int nsteps = nck * nt;
   int s = 0;
   for (int ck = 0; ck < nck; ++ck) {
     const int p = ck & 1;
@@ -207,7 +206,6 @@ __global__ __launch_bounds__(512, 1) void convt_s2_x3_kernel(const ConvTArgs a) 
     }
     __syncthreads();
   }
-  (void)nsteps;
 
   // ---- epilogue: BN scale / bias, ReLU, NHWC stores ------------------------------------------------
   const int py = cls >> 1, px = cls & 1;
