@@ -26,8 +26,8 @@
 //            per wave, no staging registers) into a 2-slot ring (padded slots: conflict-free patch
 //            reads), requested after component 6 of chunk ck;
 //     T    : the transform of chunk ck + 1, interleaved with M(ck) (its steps sit in the MFMA gaps of
-//            each component): waves 0..3 own columns v = 0..3 of the 6x6 transform, waves 4 / 6 and
-//            5 / 7 columns 4 and 5 (each pair splitting the column's 6 outputs); lane (tile, channel
+//            each component): waves 0..5 own columns v = 0..5 of the 6x6 transform (waves 6, 7
+//            only multiply; KRRN_W4_TSPLIT); lane (tile, channel
 //            half h) forms e[r] = B_v(d[r][.]) for the 6 patch rows, then V[u][v] = B_u(e[.]), splits
 //            each into the three bf16 terms and writes the MFMA operand chain [V_m V_h | V_l]
 //            (b128 + b64) to a 2-slot V buffer; V[comp][h][tile] = lane order, so the consumer's read
@@ -71,6 +71,12 @@ constexpr unsigned kOOB = 0xFFFF0000u;
 // 4 no transform, 8 no raw staging after the prologue, 16 no epilogue, 32 no output stores
 #ifndef KRRN_W4_EXP
 #define KRRN_W4_EXP 0
+#endif
+#ifndef KRRN_W4_TSPLIT
+// 0 (default): waves 0-5 own transform columns 0-5, waves 6, 7 skip the transform; 1: waves 4 / 6 and
+// 5 / 7 split columns 4 / 5 (each SIMD the same transform VALU, but both waves of a pair redo the
+// column's row steps): 0.9 % slower under sustained load (760 vs 753 us per 120-px launch)
+#define KRRN_W4_TSPLIT 0
 #endif
 #ifndef KRRN_W4_TRACE
 #define KRRN_W4_TRACE 0  // 1: per-wave cycle stamps of the first 256 blocks (profiles/w4_trace.py; timing study only)
@@ -383,8 +389,13 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   // balanced over the SIMDs (waves w and w + 4 share one): waves 0..3 transform columns 0..3 whole,
   // waves 4 / 6 column 4 and waves 5 / 7 column 5, each pair splitting its 6 outputs (u < 3 / u >= 3)
   // and both doing the column's 6 row steps: 326 + 211 VALU per SIMD instead of 326 + 326 / 326
+#if KRRN_W4_TSPLIT
   const int tv = wave < 4 ? wave : 4 + (wave & 1);
   const int tulo = wave < 6 ? 0 : 3, tuhi = wave < 4 ? 6 : (wave < 6 ? 3 : 6);
+#else
+  const int tv = wave < 6 ? wave : 5;  // waves 6, 7 skip the transform
+  const int tulo = 0, tuhi = 6;
+#endif
   int tcol[4];
   float tk[4];
   switch (tv) {
@@ -446,7 +457,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
   // one chunk: M(ck) on V[ck & 1], interleaved with T(ck + 1) into V[(ck + 1) & 1]; the raw input
   // of chunk ck + 2 goes into the ring slot T(ck) has read
   auto do_chunk = [&](int ck) {
-    const bool tr = !(KRRN_W4_EXP & 4) && ck + 1 < nck;  // the last chunk: no T
+    const bool tr = !(KRRN_W4_EXP & 4) && ck + 1 < nck && (KRRN_W4_TSPLIT || wave < 6);  // the last chunk: no T
     const int p = ck & 1;
     const char* vm = smem + p * (kVMH * 4) + 16 * lane;
     const char* vlo = smem + kOffL + p * (kVL * 4) + 8 * lane;
@@ -509,7 +520,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
-  if (!(KRRN_W4_EXP & 4)) {
+  if (!(KRRN_W4_EXP & 4) && (KRRN_W4_TSPLIT || wave < 6)) {
     t_begin(0);
 #pragma unroll
     for (int st = 0; st < 12; ++st) t_step(st);
