@@ -309,6 +309,8 @@ def convT_weights_x3(spec: "ConvSpec") -> Tuple[torch.Tensor, "ctypes.Array"]:
     U [cin_p / 8][class * 4 + tap][N][8] f32 (zero for a class's missing taps) split into the
     wino_weights_x3 planes, and the 4 x 5 int table [tap count, (dy + 1) * 3 + (dx + 1) ...]."""
     N, cin_p = spec.wt[0].shape[0], spec.cin_p
+    if spec.kind != "convT" or cin_p % 8 or len(spec.taps) != 4 or any(len(t) > 4 for t in spec.taps):
+        raise ValueError("convT_weights_x3: a stride-2 transposed conv with cin_p % 8 == 0 and <= 4 taps per class")
     nck = cin_p // 8
     U = torch.zeros(nck, 16, N, 8, device=spec.wt[0].device)
     table = (ctypes.c_int * 20)()
