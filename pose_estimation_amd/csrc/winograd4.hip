@@ -68,7 +68,8 @@ constexpr int kVL = 36 * 64 * 2;                  // u32 per V buffer, plane [V_
 constexpr int kET = kN * 4;                       // epilogue bytes per (component, tile): [64 n] f32
 constexpr unsigned kOOB = 0xFFFF0000u;
 // timing experiments only (results wrong; profiles/build_variant.sh), a bit mask: 1 no MFMAs, 2 no weight reloads,
-// 4 no transform, 8 no raw staging after the prologue, 16 no epilogue, 32 no output stores
+// 4 no transform, 8 no raw staging after the prologue, 16 no epilogue, 32 no output stores,
+// 64 one transform tap read per patch row (the VALU unchanged)
 #ifndef KRRN_W4_EXP
 #define KRRN_W4_EXP 0
 #endif
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     twm = smem + p * (kVMH * 4) + tv * 1024 + 16 * lane;
     twl = smem + kOffL + p * (kVL * 4) + tv * 512 + 8 * lane;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) td[t] = *reinterpret_cast<const f32x4*>(tb[t]);
+    for (int t = 0; t < 4; ++t) td[t] = *reinterpret_cast<const f32x4*>(tb[(KRRN_W4_EXP & 64) ? 0 : t]);
   };
   // step s < 6: e[s] from row s's taps, then row s + 1's reads; step 6 + u: output u
   auto t_step = [&](int s) {
@@ -431,7 +432,14 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
         te[s][e] = __builtin_fmaf(tk[3], td[3][e], __builtin_fmaf(tk[2], td[2][e], __builtin_fmaf(tk[1], td[1][e], tk[0] * td[0][e])));
       if (s < 5) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) td[t] = *reinterpret_cast<const f32x4*>(tb[t] + (s + 1) * kRS * 16);
+        for (int t = 0; t < 4; ++t) {
+          if ((KRRN_W4_EXP & 64) && t > 0) {  // timing study: one tap read per row, VALU unchanged
+            td[t] = td[0];
+            asm volatile("" : "+v"(td[t]));
+          } else {
+            td[t] = *reinterpret_cast<const f32x4*>(tb[t] + (s + 1) * kRS * 16);
+          }
+        }
       }
       return;
     }
