@@ -54,6 +54,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
 typedef unsigned u32x6 __attribute__((ext_vector_type(6)));
 
 constexpr int kGX = 16, kGY = 2, kT = kGX * kGY;  // tiles per block
@@ -79,6 +80,14 @@ constexpr unsigned kOOB = 0xFFFF0000u;
 // column's row steps): 0.9 % slower under sustained load (760 vs 753 us per 120-px launch)
 #define KRRN_W4_TSPLIT 0
 #endif
+#ifndef KRRN_W4_TPAIR
+// 1: waves 2 pr + h (pr < 3) transform the column pair (2 pr, 2 pr + 1) of channel half h, one channel
+// pair per lane: 5 ds_read_b64 per patch row shared by both columns instead of 4 ds_read_b128 per column
+// (-37 % transform LDS-array cycles, but 6 ds_write_b32 per output for 2): 0.8 % slower under sustained
+// load (762 / 765 vs 756 / 759 us per 120-px launch, profiles/r6_tpair_ab.txt), so 0 (default)
+#define KRRN_W4_TPAIR 0
+#endif
+static_assert(!(KRRN_W4_TPAIR && KRRN_W4_TSPLIT), "one transform split");
 #ifndef KRRN_W4_TRACE
 #define KRRN_W4_TRACE 0  // 1: per-wave cycle stamps of the first 256 blocks (profiles/w4_trace.py; timing study only)
 #endif
@@ -146,12 +155,20 @@ __device__ __forceinline__ bf16x8 sub4(const u32x6& c, int o) {
   return __builtin_bit_cast(bf16x8, u32x4{c[o], c[o + 1], c[o + 2], c[o + 3]});
 }
 
-// row K of B^T applied to x[0..5] (scalar f32, element-wise over the 4 channels)
-template <int K>
-__device__ __forceinline__ f32x4 bt_row(const f32x4 (&x)[6]) {
-  f32x4 y;
+// x (a channel pair) -> its packed bf16 terms {m, h, l}
+__device__ __forceinline__ u32x3 split3_pair(const f32x2 x) {
+  const unsigned hh = pk_bf16(x[0], x[1]);
+  const float r0 = x[0] - bf_lo(hh), r1 = x[1] - bf_hi(hh);
+  const unsigned m = pk_bf16(r0, r1);
+  return u32x3{m, hh, pk_bf16(r0 - bf_lo(m), r1 - bf_hi(m))};
+}
+
+// row K of B^T applied to x[0..5] (scalar f32, element-wise over the vector's channels)
+template <int K, typename V>
+__device__ __forceinline__ V bt_row(const V (&x)[6]) {
+  V y;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < (int)(sizeof(V) / 4); ++e) {
     if constexpr (K == 0) y[e] = __builtin_fmaf(4.f, x[0][e], __builtin_fmaf(-5.f, x[2][e], x[4][e]));
     if constexpr (K == 1) y[e] = __builtin_fmaf(-4.f, x[1][e] + x[2][e], x[3][e] + x[4][e]);
     if constexpr (K == 2) y[e] = __builtin_fmaf(4.f, x[1][e] - x[2][e], x[4][e] - x[3][e]);
@@ -383,6 +400,80 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
 
+#if KRRN_W4_TPAIR
+  // T, column pairs: wave 2 pr + th (pr < 3) transforms columns 2 pr and 2 pr + 1 of channel half th;
+  // lane (tile = lane >> 1, channel pair tq = lane & 1) reads 5 taps per patch row as f32x2 (one tile
+  // row per 32-lane ds_read_b64 group: 16 slots 36 dwords apart x 2 halves, conflict-free) in an order
+  // where column 2 pr takes taps 0..3 and column 2 pr + 1 taps 1..4 (the pair (2, 3) reads tap 1 twice),
+  // and writes each output's m / h / l bf16 pairs into the consumer's chain entry (16 tiles x 2 pairs
+  // per 32-lane ds_write_b32 group: 2-way, free)
+  const int tpr = wave < 6 ? wave >> 1 : 0, th = wave & 1;
+  const int ttile = lane >> 1, tq = lane & 1;
+  int tcol[5];
+  float ka[4], kb[4];
+  switch (tpr) {
+    case 0:  // 4 d0 - 5 d2 + d4 | -4 (d1 + d2) + d3 + d4
+      tcol[0] = 0; tcol[1] = 2; tcol[2] = 4; tcol[3] = 1; tcol[4] = 3;
+      ka[0] = 4.f; ka[1] = -5.f; ka[2] = 1.f; ka[3] = 0.f; kb[0] = -4.f; kb[1] = 1.f; kb[2] = -4.f; kb[3] = 1.f;
+      break;
+    case 1:  // 4 (d1 - d2) + d4 - d3 | 2 (d3 - d1) + d4 - d2
+      tcol[0] = 1; tcol[1] = 2; tcol[2] = 3; tcol[3] = 4; tcol[4] = 1;
+      ka[0] = 4.f; ka[1] = -4.f; ka[2] = -1.f; ka[3] = 1.f; kb[0] = -1.f; kb[1] = 2.f; kb[2] = 1.f; kb[3] = -2.f;
+      break;
+    default:  // 2 (d1 - d3) + d4 - d2 | 4 d1 - 5 d3 + d5
+      tcol[0] = 2; tcol[1] = 4; tcol[2] = 1; tcol[3] = 3; tcol[4] = 5;
+      ka[0] = -1.f; ka[1] = 1.f; ka[2] = 2.f; ka[3] = -2.f; kb[0] = 0.f; kb[1] = 4.f; kb[2] = -5.f; kb[3] = 1.f;
+      break;
+  }
+  const int pbase = (4 * (ttile >> 4)) * kRS + 9 * (ttile & 15) + th;  // patch origin slot
+  const char* tb[5];
+  char* twm = nullptr;  // this lane's word in the V entry of component 2 pr (plane MH)
+  char* twl = nullptr;  // (plane L)
+  f32x2 td[5], tea[6], teb[6];
+  auto t_begin = [&](int ck) {
+    const int p = ck & 1;
+    const char* rb = smem + kOffR + p * (kRingF * 4) + 16 * pbase + 8 * tq;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) tb[t] = rb + 16 * (2 * tcol[t] + (tcol[t] >> 2));
+    twm = smem + p * (kVMH * 4) + 2 * tpr * 1024 + 16 * (32 * th + ttile) + 4 * tq;
+    twl = smem + kOffL + p * (kVL * 4) + 2 * tpr * 512 + 8 * (32 * th + ttile) + 4 * tq;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) td[t] = *reinterpret_cast<const f32x2*>(tb[t]);
+  };
+  auto t_step = [&](int s) {
+    if (s < 6) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        tea[s][e] = __builtin_fmaf(ka[3], td[3][e], __builtin_fmaf(ka[2], td[2][e], __builtin_fmaf(ka[1], td[1][e], ka[0] * td[0][e])));
+        teb[s][e] = __builtin_fmaf(kb[3], td[4][e], __builtin_fmaf(kb[2], td[3][e], __builtin_fmaf(kb[1], td[2][e], kb[0] * td[1][e])));
+      }
+      if (s < 5) {
+#pragma unroll
+        for (int t = 0; t < 5; ++t) td[t] = *reinterpret_cast<const f32x2*>(tb[t] + (s + 1) * kRS * 16);
+      }
+      return;
+    }
+    const int u = s - 6;
+    f32x2 xa, xb;
+    switch (u) {
+      case 0: xa = bt_row<0>(tea); xb = bt_row<0>(teb); break;
+      case 1: xa = bt_row<1>(tea); xb = bt_row<1>(teb); break;
+      case 2: xa = bt_row<2>(tea); xb = bt_row<2>(teb); break;
+      case 3: xa = bt_row<3>(tea); xb = bt_row<3>(teb); break;
+      case 4: xa = bt_row<4>(tea); xb = bt_row<4>(teb); break;
+      default: xa = bt_row<5>(tea); xb = bt_row<5>(teb); break;
+    }
+    const u32x3 ca = split3_pair(xa), cb = split3_pair(xb);
+    char* wm = twm + 6 * u * 1024;
+    char* wl = twl + 6 * u * 512;
+    *reinterpret_cast<unsigned*>(wm) = ca[0];
+    *reinterpret_cast<unsigned*>(wm + 8) = ca[1];
+    *reinterpret_cast<unsigned*>(wl) = ca[2];
+    *reinterpret_cast<unsigned*>(wm + 1024) = cb[0];
+    *reinterpret_cast<unsigned*>(wm + 1024 + 8) = cb[1];
+    *reinterpret_cast<unsigned*>(wl + 512) = cb[2];
+  };
+#else
   // T: wave tv = wave < 6 transforms column tv of every (tile, channel half) patch: lane (tile, h)
   // forms e[r] = B_tv(d[r][.]) over the 6 patch rows (the row's taps: up to 4 columns with
   // wave-uniform coefficients), then V[u][tv] = B_u(e) for u = 0..5, split into the operand chain
@@ -458,6 +549,7 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
     *reinterpret_cast<u32x4*>(twm + 6 * u * 1024) = u32x4{ch[0], ch[1], ch[2], ch[3]};
     *reinterpret_cast<u32x2*>(twl + 6 * u * 512) = u32x2{ch[4], ch[5]};
   };
+#endif
   // which transform steps run after component k's MFMAs (the VALU work beside the matrix pipe)
   constexpr int kStep0[10] = {0, 1, 2, 3, 4, 5, 7, 9, 11, 12};  // steps kStep0[k] .. kStep0[k + 1] - 1
 
