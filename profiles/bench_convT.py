@@ -2,8 +2,9 @@
 128 -> 128, both 30 -> 60 px, B = 64) as one grouped split-bf16 launch per tile shape, built the
 way hrnet.emit_conv builds them (parity classes, channel-chunk k order).
 
-usage (GPU box): python3 profiles/bench_convT.py   (TILES=1,6,8 the grouped tiles; "s2" = the
-all-classes-per-block kernel, krrn_convT_s2_x3_f32)
+usage (GPU box): python3 profiles/bench_convT.py   (TILES=1,6,8 the grouped tiles, TILES= none; "s2" = the
+all-classes-per-block kernel, krrn_convT_s2_x3_f32; CASE=0 / 1 one of the two convs, e.g. for a
+per-conv rocprofv3 --pmc pass)
 """
 import os
 import sys
@@ -50,6 +51,8 @@ def ev_time(fn, reps=20):
     return a.elapsed_time(b) / reps
 
 
+if os.environ.get("CASE"):
+    cases = [cases[int(os.environ["CASE"])]]
 for name, conv in cases:
     g = torch.Generator().manual_seed(0)
     with torch.no_grad():
@@ -59,7 +62,7 @@ for name, conv in cases:
     xa.t.copy_(torch.randn(xa.t.shape, generator=g).to(dev))
     out = ops.new_act(B, 60, 60, spec.cout, dev)
     line, ref = name + ":", None
-    for tile in [int(t) for t in os.environ.get("TILES", "1,6,8").split(",")]:
+    for tile in [int(t) for t in os.environ.get("TILES", "1,6,8").split(",") if t]:
         for q in (0, 16):
             try:
                 plan = build(spec, xa, out, tile, q)
@@ -81,6 +84,6 @@ for name, conv in cases:
                                                    60, 60, P(torch.cuda.current_stream().cuda_stream)), "convT_s2")
     ms = ev_time(s2)
     got = out.t.clone()
-    err = float((got - ref).abs().max() / ref.abs().max())
+    err = float((got - ref).abs().max() / ref.abs().max()) if ref is not None else float("nan")
     line += f" | s2 {ms * 1e3:6.1f} us ({err:.1e})"
     print(line, flush=True)
