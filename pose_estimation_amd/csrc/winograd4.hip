@@ -125,14 +125,10 @@ struct Wino4Args {
   float* part;
 };
 
-// sum over the 16 lanes of a DPP row (every lane gets the sum): quad swaps, then half-row and row
-// mirrors (winograd.hip's head epilogue)
-__device__ __forceinline__ float row16_sum(float x) {
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));  // quad [1 0 3 2]
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));  // quad [2 3 0 1]
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));  // row_mirror
-  return x;
+// x of the lane the DPP control names (within a row of 16 lanes)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
@@ -204,7 +200,7 @@ __device__ __forceinline__ constexpr bool at_uses(int u) {
 
 // epilogue: output row I of local tile tl (of the pass's 16), channels ng .. ng + 3;
 // E = [36][16 tiles][64 n] f32
-template <int I, bool HEAD>
+template <int I, int HP>
 __device__ __forceinline__ void epi_row(const Wino4Args& a, const char* E, int nq, int tl, int pass, int b, int ty0,
                                         int tx0, int ng, int nb) {
   const char* eb = E + tl * kET + nq * 16;
@@ -227,18 +223,18 @@ __device__ __forceinline__ void epi_row(const Wino4Args& a, const char* E, int n
   const int ty = ty0 + (tile >> 4), tx = tx0 + (tile & 15);
   const int oy = 4 * ty + I;
   const int nj = min(4, a.W - 4 * tx);  // output columns of this tile inside the image
-  if constexpr (HEAD) {
+  if constexpr (HP > 0) {
     // the 16 lanes of a DPP row are the 16 channel quads of one tile: every lane takes part in the
     // row sums (no early exit), invalid pixels / channels contribute zeros
     const bool ok = ty < a.Ht && oy < a.H && nj > 0 && ng < a.n_store;  // n_store = N % 4 == 0
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     const f32x4 scl = ok && a.scale ? *reinterpret_cast<const f32x4*>(a.scale + ng) : f32x4{1.f, 1.f, 1.f, 1.f};
     const f32x4 bia = ok && a.bias ? *reinterpret_cast<const f32x4*>(a.bias + ng) : zero;
-    f32x4 w[4];
+    f32x4 w[HP];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) w[o] = ok ? *reinterpret_cast<const f32x4*>(a.w1 + (size_t)o * a.N + ng) : zero;
+    for (int o = 0; o < HP; ++o) w[o] = ok ? *reinterpret_cast<const f32x4*>(a.w1 + (size_t)o * a.N + ng) : zero;
     const long long pix = ((long long)b * a.H + oy) * a.W + 4 * tx;
-    float sum[4][4];
+    float s[4][HP];  // this lane's 4-channel partial dot of pixel j with w1 row o
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bool okj = ok && j < nj;
@@ -252,14 +248,35 @@ __device__ __forceinline__ void epi_row(const Wino4Args& a, const char* E, int n
       }
       if (!okj) v = zero;
 #pragma unroll
-      for (int o = 0; o < 4; ++o) sum[j][o] = row16_sum(v[0] * w[o][0] + v[1] * w[o][1] + v[2] * w[o][2] + v[3] * w[o][3]);
+      for (int o = 0; o < HP; ++o) s[j][o] = v[0] * w[o][0] + v[1] * w[o][1] + v[2] * w[o][2] + v[3] * w[o][3];
     }
-    if (nq != 0 || !(ty < a.Ht && oy < a.H && nj > 0)) return;
-    const long long M = (long long)a.B * a.H * a.W;
+    // sum over the 16 channel quads as a reduce-scatter: two exchange levels leave lane nq the 4-lane
+    // partials of pixel j = nq & 3 (the partner gets the other half of the values), two rotations
+    // of the DPP row then add the 4 lanes of each class
+    const bool b0 = nq & 1, b1 = (nq >> 1) & 1;
+    float t1[2][HP];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j < nj)
-        *reinterpret_cast<f32x4*>(a.part + ((size_t)nb * M + pix + j) * 4) = f32x4{sum[j][0], sum[j][1], sum[j][2], sum[j][3]};
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int o = 0; o < HP; ++o) {
+        const float keep = b0 ? s[2 * jj + 1][o] : s[2 * jj][o], send = b0 ? s[2 * jj][o] : s[2 * jj + 1][o];
+        t1[jj][o] = keep + dpp_f<0xB1>(send);  // quad [1 0 3 2]
+      }
+    float t2[HP];
+#pragma unroll
+    for (int o = 0; o < HP; ++o) {
+      const float keep = b1 ? t1[1][o] : t1[0][o], send = b1 ? t1[0][o] : t1[1][o];
+      t2[o] = keep + dpp_f<0x4E>(send);  // quad [2 3 0 1]
+      t2[o] += dpp_f<0x128>(t2[o]);      // row_ror 8
+      t2[o] += dpp_f<0x124>(t2[o]);      // row_ror 4
+    }
+    const int j = nq & 3;
+    if (nq >= 4 || !(ty < a.Ht && oy < a.H && j < nj)) return;
+    const long long M = (long long)a.B * a.H * a.W;
+    f32x4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int o = 0; o < HP; ++o) r[o] = t2[o];
+    *reinterpret_cast<f32x4*>(a.part + ((size_t)nb * M + pix + j) * 4) = r;
     return;
   }
   if (ty >= a.Ht || oy >= a.H || nj <= 0 || ng >= a.n_store) return;
@@ -327,7 +344,7 @@ __device__ unsigned g_w4_trace[256 * 8 * kTrN];
   } while (0)
 #endif
 
-template <bool HEAD>
+template <int HP>  // 0: conv output stored; 1..4: head form, HP rows of w1
 __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -672,10 +689,10 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
       const int tl = 4 * ((wave >> 2) + 2 * it) + etl;
       const int ng = n0 + 4 * enq;
       switch (ei) {
-        case 0: epi_row<0, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
-        case 1: epi_row<1, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
-        case 2: epi_row<2, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
-        default: epi_row<3, HEAD>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
+        case 0: epi_row<0, HP>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
+        case 1: epi_row<1, HP>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
+        case 2: epi_row<2, HP>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
+        default: epi_row<3, HP>(a, smem, enq, tl, pass, b, ty0, tx0, ng, nb); break;
       }
     }
     __syncthreads();
@@ -722,7 +739,7 @@ KRRN_API int krrn_conv3x3_wino4_x3_f32(const float* in, int in_cs, int in_co, in
   if (a.img * 4 >= 0x7FFF0000LL || nrec * 16 >= 0x7FFF0000LL) return KRRN_ESHAPE;
   const long long rb = (long long)B * krrn_cdiv(a.Ht, kGY) * krrn_cdiv(a.Wt, kGX) * krrn_cdiv(N, kN);
   if (rb > 0x7fffffffLL) return KRRN_ESHAPE;
-  hipLaunchKernelGGL(wino_f43_x3_kernel<false>, dim3((unsigned)rb), dim3(512), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(wino_f43_x3_kernel<0>, dim3((unsigned)rb), dim3(512), 0, (hipStream_t)stream, a);
   return krrn_launch_status();
 }
 
@@ -754,7 +771,9 @@ KRRN_API int krrn_conv3x3_wino4_x3_head_f32(const float* in, int in_cs, int in_c
   const long long fb = (M + 255) / 256;
   if (rb > 0x7fffffffLL || fb > 0x7fffffffLL) return KRRN_ESHAPE;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wino_f43_x3_kernel<true>, dim3((unsigned)rb), dim3(512), 0, s, a);
+  // p1 <= 3 (nml_final of one class) forms 3 dot products per pixel, p1 = 4 all four
+  if (p1 <= 3) hipLaunchKernelGGL(wino_f43_x3_kernel<3>, dim3((unsigned)rb), dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(wino_f43_x3_kernel<4>, dim3((unsigned)rb), dim3(512), 0, s, a);
   const int st = krrn_launch_status();
   if (st != KRRN_OK) return st;
   hipLaunchKernelGGL(wino4_head_finish_kernel, dim3((unsigned)fb), dim3(256), 0, s, part, nbn, M, H * W, b1, p1, out,

@@ -21,7 +21,7 @@ def _short(name: str) -> str:
     m = re.search(r"conv_group_kernel<(\d+), (\d+), (\d+), \d+>", name)
     if m:
         return f"conv_group<{m.group(1)},{m.group(2)},{m.group(3)}>"
-    if "wino_f43_x3_kernel<true>" in name:
+    if re.search(r"wino_f43_x3_kernel<(true|[1-4])>", name):
         return "wino_f43_x3_head"
     if "wino_f43_x3" in name:
         return "wino_f43_x3"
