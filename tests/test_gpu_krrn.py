@@ -247,6 +247,42 @@ def test_config2_full_batch(models, dev):
         print(f"  B=64 vs B=2 argmax({name}) mismatches: {n_bad}")
 
 
+def test_batch_composition_invariance(models, dev):
+    """At a fixed batch size a crop's results do not depend on the other crops of the batch: the
+    B = 64 config-2 plan run twice, with crops 1..62 replaced by other crops the second time, gives
+    crops 0 and 63 bit for bit the same maps, fusion kNN decisions and pred_t (no cross-crop
+    reduction, split or shared scratch anywhere on the path; the pool permutations are shared by
+    the batch in both runs, gcn3d.py:239)."""
+    m, _ = models
+    B, S, N = 64, 120, 1000
+    d = make_batch(B, S, N, seed=41)
+    other = make_batch(B, S, N, seed=42)
+    perms = [p.to(dev) for p in _draw_perms(N, 17)]
+
+    def run(batch):
+        o = m(batch["img_croped"].to(dev), batch["cloud"].to(dev), batch["choose"].to(dev),
+              batch["cls_id"].to(dev), perms=perms)
+        torch.cuda.synchronize()
+        fb = m.get_plan(B, S, N, True).fusion_bufs
+        return ({k: v.detach().clone().cpu() for k, v in o.items() if torch.is_tensor(v)},
+                {k: fb[k].clone().cpu() for k in _DECISIONS})
+
+    out1, dec1 = run(d)
+    mixed = {k: v.clone() for k, v in d.items()}
+    for k in ("img_croped", "cloud", "choose", "cls_id"):
+        mixed[k][1:63] = other[k][1:63]
+    out2, dec2 = run(mixed)
+    keep = [0, 63]
+    for k, v in out1.items():
+        if v.dim() > 0 and v.shape[0] == B:
+            assert torch.equal(v[keep], out2[k][keep]), k
+    for k in ("xyz", "pred_t"):
+        assert not torch.equal(out1[k][1:63], out2[k][1:63]), k  # the other crops did change
+    for k in _DECISIONS:
+        assert torch.equal(dec1[k][keep], dec2[k][keep]), k
+    print(f"  crops 0 / 63 identical across batch contents: {sorted(k for k, v in out1.items() if v.shape[:1] == (B,))}")
+
+
 def test_opt_pose_false(models, dev):
     m, o = models
     d = make_batch(1, 80, 300, seed=5)
