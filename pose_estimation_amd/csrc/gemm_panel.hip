@@ -31,6 +31,11 @@ constexpr int kPanelMaxN = 2048;  // columns whose bias a block stages in LDS
 #ifndef KRRN_GP_EXP
 #define KRRN_GP_EXP 0  // timing experiments only (results wrong): 1 no output stores, 2 no MFMAs
 #endif
+#ifndef KRRN_GP_NW128
+// waves (32-row panels) per block at K = 128: 4 (two blocks per CU) or 8 (one; half the weight-tile
+// copies into LDS, measured no faster: DESIGN.md "Next (after round 6)")
+#define KRRN_GP_NW128 4
+#endif
 
 typedef __bf16 gp_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 gp_bf16x2 __attribute__((ext_vector_type(2)));
@@ -80,20 +85,20 @@ typedef __attribute__((address_space(3))) void gp_lds_void;
 // stores per tile (the vmcnt(4) accounting below depends on it).
 constexpr int kTP = 36;  // LDS pitch of a transposed tile row (floats; conflict-free b128 writes)
 
-template <int KT, bool RES>
-__global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g) {
+template <int KT, bool RES, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_pdma_x3_kernel(const PanelArgs g) {
   constexpr int G = KT / 8;
   constexpr int TILE_U32 = G * 384;
-  constexpr int NI = TILE_U32 / 256 / 4;  // 1-KB DMA instructions per wave and tile
-  static_assert(NI * 4 * 256 == TILE_U32, "tile DMA split");
+  constexpr int NI = TILE_U32 / 256 / NW;  // 1-KB DMA instructions per wave and tile
+  static_assert(NI * NW * 256 == TILE_U32, "tile DMA split");
   __shared__ __attribute__((aligned(16))) unsigned sbA[TILE_U32];
   __shared__ __attribute__((aligned(16))) unsigned sbB[TILE_U32];
   __shared__ __attribute__((aligned(16))) float sbias[kPanelMaxN];  // read as f32x4 (ds_read_b128)
-  __shared__ __attribute__((aligned(16))) float stile[4][32 * kTP];
+  __shared__ __attribute__((aligned(16))) float stile[NW][32 * kTP];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nl = lane & 31, fh = lane >> 5;
-  const int m0 = blockIdx.x * 128 + wave * 32;
+  const int m0 = blockIdx.x * (32 * NW) + wave * 32;
 
   gp_u32x8 ca[G];
   {
@@ -118,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void gemm_pdma_x3_kernel(const PanelArgs g)
 
   const int ct0 = blockIdx.y * g.ntile_per_split;
   const int ct1 = min(ct0 + g.ntile_per_split, g.N >> 5);
-  for (int n = ct0 * 32 + tid; n < ct1 * 32; n += 256) sbias[n] = g.bias ? g.bias[n] : 0.f;
+  for (int n = ct0 * 32 + tid; n < ct1 * 32; n += 64 * NW) sbias[n] = g.bias ? g.bias[n] : 0.f;
   // this wave's NI 1-KB pieces of tile ct: byte offset (ct * TILE_U32 + (wave * NI + i) * 256) * 4,
   // through a buffer resource (per-lane 32-bit voffset, the tile part in soffset: no 64-bit address
   // registers)
@@ -255,9 +260,11 @@ KRRN_API int krrn_gemm_panel_x3_f32(const float* a, int lda, int M, int K, int N
   g.vec = krrn_aligned16(out) && !(ldo & 3) && (!res || (krrn_aligned16(res) && !(ldr & 3))) &&
           (!bias || krrn_aligned16(bias)) ? 1 : 0;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)krrn_cdiv(M, 128), (unsigned)krrn_cdiv(ntiles, per));
-  if (K == 128) hipLaunchKernelGGL((gemm_pdma_x3_kernel<128, false>), grid, dim3(256), 0, s, g);
-  else if (res) hipLaunchKernelGGL((gemm_pdma_x3_kernel<64, true>), grid, dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((gemm_pdma_x3_kernel<64, false>), grid, dim3(256), 0, s, g);
+  const unsigned gy = (unsigned)krrn_cdiv(ntiles, per);
+  if (K == 128)
+    hipLaunchKernelGGL((gemm_pdma_x3_kernel<128, false, KRRN_GP_NW128>),
+                       dim3((unsigned)krrn_cdiv(M, 32 * KRRN_GP_NW128), gy), dim3(64 * KRRN_GP_NW128), 0, s, g);
+  else if (res) hipLaunchKernelGGL((gemm_pdma_x3_kernel<64, true, 4>), dim3((unsigned)krrn_cdiv(M, 128), gy), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_pdma_x3_kernel<64, false, 4>), dim3((unsigned)krrn_cdiv(M, 128), gy), dim3(256), 0, s, g);
   return krrn_launch_status();
 }
