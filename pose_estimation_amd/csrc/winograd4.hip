@@ -91,8 +91,14 @@ static_assert(!(KRRN_W4_TPAIR && KRRN_W4_TSPLIT), "one transform split");
 #ifndef KRRN_W4_TRACE
 #define KRRN_W4_TRACE 0  // 1: per-wave cycle stamps of the first 256 blocks (profiles/w4_trace.py; timing study only)
 #endif
-constexpr int kRawK = 6;  // component slot after which the raw chunk two ahead is requested
-constexpr int kGap = 6;   // transform VALU instructions placed in each MFMA gap
+#ifndef KRRN_W4_RAWK
+#define KRRN_W4_RAWK 6
+#endif
+#ifndef KRRN_W4_GAP
+#define KRRN_W4_GAP 6
+#endif
+constexpr int kRawK = KRRN_W4_RAWK;  // component slot after which the raw chunk two ahead is requested
+constexpr int kGap = KRRN_W4_GAP;    // transform VALU instructions placed in each MFMA gap
 static_assert(kRR * kRS <= kRing && kRing == 3 * 512, "raw ring");
 static_assert(2 * (kRC - 1) + 1 + (kRC - 1) / 4 < kRS && (kRS * 4) % 16 == 0, "padded raw row");
 // LDS bytes: V plane MH x 2 | V plane L x 2 | raw ring x 2 (the epilogue's [36][64][12] f32 reuses
