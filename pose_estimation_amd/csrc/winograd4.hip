@@ -88,6 +88,11 @@ constexpr unsigned kOOB = 0xFFFF0000u;
 #define KRRN_W4_TPAIR 0
 #endif
 static_assert(!(KRRN_W4_TPAIR && KRRN_W4_TSPLIT), "one transform split");
+#ifndef KRRN_W4_SKIP3
+// 1: waves 0 / 5 skip the zero-coefficient 4th tap read of rows 1-5. The uniform branch splits the
+// chunk body's scheduling regions: 1.9 % slower under sustained load (772 vs 758 us, r6_w4_skip3_ab.txt)
+#define KRRN_W4_SKIP3 0
+#endif
 #ifndef KRRN_W4_TRACE
 #define KRRN_W4_TRACE 0  // 1: per-wave cycle stamps of the first 256 blocks (profiles/w4_trace.py; timing study only)
 #endif
@@ -550,6 +555,9 @@ __global__ __launch_bounds__(512, 1) void wino_f43_x3_kernel(const Wino4Args a) 
           if ((KRRN_W4_EXP & 64) && t > 0) {  // timing study: one tap read per row, VALU unchanged
             td[t] = td[0];
             asm volatile("" : "+v"(td[t]));
+          } else if (KRRN_W4_SKIP3 && t == 3) {
+            // columns 0 / 5 have 3 taps (tk[3] = 0): keep row 0's finite 4th tap instead of re-reading
+            if (tv >= 1 && tv <= 4) td[3] = *reinterpret_cast<const f32x4*>(tb[3] + (s + 1) * kRS * 16);
           } else {
             td[t] = *reinterpret_cast<const f32x4*>(tb[t] + (s + 1) * kRS * 16);
           }
