@@ -55,10 +55,8 @@ MODULE_STREAMS = knobs.flag("KRRN_MODULE_STREAMS")
 # ... and across stage boundaries: a stage's last module keeps its outputs on their streams, and the
 # next stage's transition conv for branch i runs on stream i after a wait on its source's stream
 STAGE_STREAMS = knobs.flag("KRRN_STAGE_STREAMS")
-CONV_X3 = knobs.flag("KRRN_CONV_X3")
-# tile of the grouped transposed convs, and their k order: channel chunks of this many channels
-# outer, taps inner (krrn_conv_desc.k_chunk; 0 = tap-major)
-CONVT_GROUP_TILE = 8
+# k order of the grouped transposed convs: channel chunks of this many channels outer, taps inner
+# (krrn_conv_desc.k_chunk; 0 = tap-major)
 CONVT_KCHUNK = 16
 
 BN_MOMENTUM = 0.1
@@ -405,39 +403,31 @@ class _Builder:
                           out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=2, osx=2, ooy=ooy,
                           oox=oox, relu=relu, cin=spec.cin, cout=spec.cout)
                      for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off))]
-            x3 = CONV_X3
             q = CONVT_KCHUNK if CONVT_KCHUNK and spec.cin_p % CONVT_KCHUNK == 0 else 0
             wts = [ops.kchunk_weights(w, len(t), spec.cin_p, q) for w, t in zip(spec.wt, spec.taps)] if q else spec.wt
             for pr in probs:
                 pr["k_chunk"] = q
-            if q and not x3:
-                for pr, w in zip(probs, wts):
-                    self.specs.append(w)
-                    pr["wt"] = ptr(w)
-            if x3:
-                for pr, cls in zip(probs, range(len(probs))):
-                    w3 = ops.conv_weights_x3(wts[cls])
-                    self.specs.append(w3)
-                    pr["wt"] = ptr(w3)
+            for pr, cls in zip(probs, range(len(probs))):
+                w3 = ops.conv_weights_x3(wts[cls])
+                self.specs.append(w3)
+                pr["wt"] = ptr(w3)
             # split-bf16: the 128x128x16 tile (profiles/bench_conv_x3.py: transposed 4x4 272 -> 128 at
             # 30 px 501 us, 3x3 128 -> 128 at 60 px 665 us, against 742 / 854 for the f32 64x64x32)
-            add_conv_group(self.plan, probs, tile=1 if x3 else CONVT_GROUP_TILE, tag=tag + "_convT", x3=x3)
+            add_conv_group(self.plan, probs, tile=1, tag=tag + "_convT", x3=True)
             return
         for cls, (taps, (ooy, oox)) in enumerate(zip(spec.taps, spec.cls_off)):
             if spec.kind == "conv":
                 Hg, Wg, in_s, osy, osx = out.H, out.W, spec.stride, 1, 1
             else:
                 Hg, Wg, in_s, osy, osx = x.H, x.W, 1, 2, 2
-            w3 = None
-            if CONV_X3:
-                w3 = ops.conv_weights_x3(spec.wt[cls])
-                self.specs.append(w3)
+            w3 = ops.conv_weights_x3(spec.wt[cls])  # split-bf16 operands (f32 accuracy)
+            self.specs.append(w3)
             add_conv(self.plan, x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=Hg,
                      Wg=Wg, in_s=in_s, taps=taps, wt=ptr(spec.wt[cls]), N=np_, n_store=np_, scale=ptr(spec.scale),
                      bias=ptr(spec.bias), res=ptr(res.t) if res is not None else None,
                      res_cs=res.cs if res is not None else 0, res_co=res.co if res is not None else 0,
                      out=ptr(out.t), out_cs=out.cs, out_co=out.co, Ho=out.H, Wo=out.W, osy=osy, osx=osx, ooy=ooy,
-                     oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag, wt3=ptr(w3) if w3 is not None else None)
+                     oox=oox, relu=relu, cin=spec.cin, cout=spec.cout, tag=tag, wt3=ptr(w3))
 
     def resize(self, x: Act, out: Act, add: Optional[Act] = None, align: bool = False, relu: bool = False):
         assert x.cp == out.cp

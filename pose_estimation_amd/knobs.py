@@ -27,8 +27,6 @@ KNOBS: Dict[str, Tuple[Optional[str], str]] = {
     "KRRN_WINO": ("1", "3x3 stride-1 convs on the Winograd kernels; 0 = the implicit-GEMM conv"),
     "KRRN_WINO_X3": ("1", "Winograd with split-bf16 MFMAs (f32 accuracy); 0 = the f32 Winograd"),
     "KRRN_WINO4": ("1", "the heads' wide 3x3 convs on the split-bf16 Winograd F(4x4, 3x3); 0 = F(2x2, 3x3)"),
-    "KRRN_CONV_X3": ("1", "implicit-GEMM / grouped transposed convs with split-bf16 MFMAs; 0 = f32 MFMAs"),
-    "KRRN_NCHW_X3": ("1", "the heads' final 1x1 on the split-bf16 kernel; 0 = the f32 kernel"),
     "KRRN_FUSE_EARLY": ("1", "HRNet fuse terms that read one branch start on that branch's stream before the join"),
     "KRRN_MODULE_STREAMS": ("1", "consecutive HRNet modules of a stage keep each branch on its stream (no barrier between them)"),
     "KRRN_STAGE_STREAMS": ("1", "with KRRN_MODULE_STREAMS, HRNet stages chain per branch stream too (transitions on their branch's stream)"),

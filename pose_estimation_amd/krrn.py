@@ -45,7 +45,6 @@ from .runtime import Late, Plan, add_conv, h2d, ptr
 
 # the wide head's final 1x1 conv (xyz_final, K = 128) on split-bf16 operands (f32 accuracy,
 # krrn_conv1x1_nchw_x3_f32) instead of f32 MFMAs
-NCHW_X3 = knobs.flag("KRRN_NCHW_X3")
 
 
 TBASE_EARLY = knobs.flag("KRRN_TBASE_EARLY")
@@ -248,7 +247,7 @@ class KRRNPlan:
         np_ = pad4(spec.cout)
         if len(spec.taps[0]) == 1 and spec.stride == 1 and spec.cin_p <= 256 and np_ <= 80:
             name, wt = "krrn_conv1x1_nchw_f32", spec.wt[0]
-            if NCHW_X3 and spec.cin_p == 128 and np_ > 48:  # split-bf16 MFMAs, weights held in registers
+            if spec.cin_p == 128 and np_ > 48:  # split-bf16 MFMAs, weights held in registers
                 name, wt = "krrn_conv1x1_nchw_x3_f32", ops.quad_weights_x3(spec.wt[0], np_, 128)
                 self.plan.buffers.append(wt)
             self.plan.add(name, ptr(x.t), x.cs, x.co, x.B, Ho * Wo, spec.cin_p, ptr(wt), np_,
