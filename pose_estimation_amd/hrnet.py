@@ -32,7 +32,6 @@ from .runtime import add_conv_group, add_gemm, Plan, add_conv, ptr
 
 # switches (pose_estimation_amd/knobs.py has each one's meaning)
 DECONV_FOLD = knobs.flag("KRRN_DECONV_FOLD")
-CONVT_GROUP = knobs.flag("KRRN_CONVT_GROUP")
 CONVT_S2 = knobs.flag("KRRN_CONVT_S2")
 SMALL_CONV = knobs.flag("KRRN_SMALL_CONV")
 GEMM_1X1 = knobs.flag("KRRN_GEMM_1X1")
@@ -394,7 +393,7 @@ class _Builder:
         if CONVT_S2 and ops.convT_s2_eligible(spec, x, out, res):
             self.emit_convT_s2(x, spec, out, relu, tag)
             return
-        if spec.kind == "convT" and CONVT_GROUP and 1 < len(spec.taps) <= 4:
+        if spec.kind == "convT" and 1 < len(spec.taps) <= 4:
             # the parity classes write disjoint output pixels: one grouped launch (no tail per class)
             probs = [dict(x=ptr(x.t), x_cs=x.cs, x_co=x.co, B=x.B, Hi=x.H, Wi=x.W, cin_p=spec.cin_p, Hg=x.H, Wg=x.W,
                           in_s=1, taps=taps, wt=ptr(spec.wt[cls]), N=np_, n_store=np_, scale=ptr(spec.scale),

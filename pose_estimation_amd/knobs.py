@@ -36,7 +36,6 @@ KNOBS: Dict[str, Tuple[Optional[str], str]] = {
     "KRRN_SMALL_CONV": ("1", "HRNet branch / fuse convs on the LDS-slab conv_small kernel; 0 = implicit GEMM"),
     "KRRN_GEMM_1X1": ("1", "stride-1 1x1 convs as plain GEMMs; 0 = implicit-GEMM conv"),
     "KRRN_CONVT_S2": ("1", "stride-2 transposed convs with 128 outputs on the all-classes-per-block kernel (convt.hip); 0 = the grouped implicit GEMM"),
-    "KRRN_CONVT_GROUP": ("1", "the transposed conv's four phase convs as one grouped launch; 0 = four"),
     "KRRN_DECONV_FOLD": ("1", "fold last_layer_2 into the deconv (272 instead of 400 input channels); "
                               "0 = the literal cat + deconv"),
     "KRRN_FUSE_ID_FIRST": ("1", "HRNet fuse sums start from the identity branch; 0 = the reference's j order"),
